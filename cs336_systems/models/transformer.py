@@ -1,0 +1,329 @@
+"""Transformer LM (pre-norm, RMSNorm, RoPE, SwiGLU, causal MHA) with MI355X kernel dispatch.
+
+Architecture and parameter layout are identical to the reference's bundled model
+(``cs336-basics/cs336_basics/model.py:22-397``) so state dicts and the on-disk checkpoint format
+(``model_config.json`` + ``model.pt``, ``model.py:312-327``) interchange. What differs is the
+execution path on GPU:
+
+* every projection is ``F.linear`` → hipBLASLt bf16 GEMM under autocast;
+* RMSNorm / RoPE / SwiGLU gate / cross-entropy are the fused HIP kernels of ``cs336_systems.ops``;
+  RMSNorm writes its output straight in the autocast dtype;
+* attention never materializes N x N and never transposes: Q/K/V stay in the ``(B, N, H, D)``
+  memory order the projections produce, RoPE writes ``(B, N, H, D)``, the HIP FlashAttention-2
+  kernels read/write strided ``(B, H, N, D)`` views of it, and the output projection consumes the
+  result as a plain ``(B, N, H*D)`` view.
+
+On CPU everything falls back to the eager reference math (naive masked softmax attention), which
+is what the CPU plumbing config of BASELINE.json exercises.
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+import math
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..utils.profiling import annotate
+
+logger = logging.getLogger(__name__)
+
+# "auto": HIP flash attention on GPU, naive on CPU; "naive": always materialize; "flash": always
+# the FA2 path (HIP on GPU, tiled PyTorch on CPU).
+_ATTN_IMPL = os.environ.get("CS336_ATTN_IMPL", "auto")
+
+
+def set_attention_impl(name: str) -> None:
+    global _ATTN_IMPL
+    if name not in ("auto", "naive", "flash"):
+        raise ValueError(name)
+    _ATTN_IMPL = name
+
+
+def get_attention_impl() -> str:
+    return _ATTN_IMPL
+
+
+def _trunc_normal(shape, std, device=None, dtype=None):
+    t = torch.empty(shape, device=device, dtype=dtype or torch.float32)
+    return nn.init.trunc_normal_(t, std=std, a=-3 * std, b=3 * std)
+
+
+class Linear(nn.Module):
+    """Bias-free linear, weight ``(d_out, d_in)``, trunc-normal std sqrt(2/(d_in+d_out)) (``model.py:22-44``)."""
+
+    def __init__(self, d_in: int, d_out: int, device=None, dtype=None):
+        super().__init__()
+        std = math.sqrt(2 / (d_in + d_out))
+        self.weight = nn.Parameter(_trunc_normal((d_out, d_in), std, device, dtype), requires_grad=True)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return F.linear(x, self.weight)
+
+    def extra_repr(self):
+        return f"d_out={self.weight.shape[0]}, d_in={self.weight.shape[1]}"
+
+
+class Embedding(nn.Module):
+    """Token embedding table ``(vocab, d_model)``, trunc-normal std 1 (``model.py:47-60``)."""
+
+    def __init__(self, vocab_size: int, d_model: int, device=None, dtype=None):
+        super().__init__()
+        self.weight = nn.Parameter(_trunc_normal((vocab_size, d_model), 1.0, device, dtype), requires_grad=True)
+
+    def forward(self, token_ids: torch.Tensor) -> torch.Tensor:
+        return F.embedding(token_ids, self.weight)
+
+    def extra_repr(self):
+        return f"vocab_size={self.weight.shape[0]}, d={self.weight.shape[1]}"
+
+
+class RMSNorm(nn.Module):
+    """RMSNorm (``model.py:63-110``); HIP kernel on GPU (``csrc/ops/rmsnorm.hip``)."""
+
+    def __init__(self, hidden_size: int, eps: float = 1e-5, device=None, dtype=None):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(hidden_size, device=device, dtype=dtype))
+        self.eps = eps
+
+    def forward(self, x):
+        return ops.rmsnorm(x, self.weight, self.eps)
+
+    def extra_repr(self):
+        return f"hidden_size={self.weight.shape[0]}, eps={self.eps}"
+
+
+class RotaryEmbedding(nn.Module):
+    """RoPE with a ``(2, ctx, d/2)`` cos/sin cache (``model.py:113-150``)."""
+
+    def __init__(self, context_length: int, dim: int, theta: float = 10000.0, device=None):
+        super().__init__()
+        self.register_buffer("_freq_cis_cache", RotaryEmbedding._init_cache(context_length, dim, theta, device), persistent=False)
+
+    @staticmethod
+    def _init_cache(context_length: int, dim: int, theta: float, device=None) -> torch.Tensor:
+        assert dim % 2 == 0
+        d = torch.arange(0, dim, 2, device=device) / dim
+        freqs = theta**-d
+        t = torch.arange(context_length, device=device)
+        freqs = torch.outer(t, freqs)
+        return torch.stack((torch.cos(freqs), torch.sin(freqs)))
+
+    @property
+    def cos(self):
+        return self._freq_cis_cache[0]
+
+    @property
+    def sin(self):
+        return self._freq_cis_cache[1]
+
+    def forward(self, x: torch.Tensor, pos_ids: torch.Tensor | None = None) -> torch.Tensor:
+        return ops.rope(x, self.cos, self.sin, pos_ids)
+
+    def extra_repr(self):
+        return f"context_length={self._freq_cis_cache.shape[1]}, dim/2={self._freq_cis_cache.shape[2]}"
+
+
+def silu(x: torch.Tensor) -> torch.Tensor:
+    return x * torch.sigmoid(x)
+
+
+class SwiGLU(nn.Module):
+    """``w2(silu(w1 x) * w3 x)`` (``model.py:389-397``); the gate is one HIP kernel on GPU."""
+
+    def __init__(self, d_model: int, d_ff: int, device=None, dtype=None):
+        super().__init__()
+        self.w1 = Linear(d_model, d_ff, device, dtype)
+        self.w2 = Linear(d_ff, d_model, device, dtype)
+        self.w3 = Linear(d_model, d_ff, device, dtype)
+
+    def forward(self, x):
+        return self.w2(ops.silu_mul(self.w1(x), self.w3(x)))
+
+
+def softmax(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
+    rescaled = x - torch.max(x, dim=dim, keepdim=True)[0]
+    e = torch.exp(rescaled)
+    return e / torch.sum(e, dim=dim, keepdim=True)
+
+
+def scaled_dot_product_attention(Q, K, V, mask=None):
+    """Materializing SDPA (``model.py:400-432``): mask==False positions get -inf."""
+    d_k = K.shape[-1]
+    scores = torch.matmul(Q, K.transpose(-1, -2)) / math.sqrt(d_k)
+    if mask is not None:
+        scores = torch.where(mask, scores, float("-inf"))
+    return torch.matmul(softmax(scores, dim=-1), V)
+
+
+class CausalMultiHeadSelfAttention(nn.Module):
+    """Causal MHA with RoPE on Q and K (``model.py:435-524``)."""
+
+    def __init__(self, d_model: int, num_heads: int, positional_encoder: RotaryEmbedding, device=None, dtype=None):
+        super().__init__()
+        assert d_model % num_heads == 0
+        self.d_model = d_model
+        self.num_heads = num_heads
+        self.d_k = d_model // num_heads
+        self.d_v = self.d_k
+        self.q_proj = Linear(d_model, num_heads * self.d_k, device, dtype)
+        self.k_proj = Linear(d_model, num_heads * self.d_k, device, dtype)
+        self.v_proj = Linear(d_model, num_heads * self.d_v, device, dtype)
+        self.output_proj = Linear(num_heads * self.d_v, d_model, device, dtype)
+        self.positional_encoder = positional_encoder
+
+    def forward(self, x: torch.Tensor, token_positions: torch.Tensor | None = None) -> torch.Tensor:
+        *b, N, d_model = x.shape
+        assert d_model == self.d_model
+        B = int(math.prod(b)) if b else 1
+        H, dk = self.num_heads, self.d_k
+        x3 = x.reshape(B, N, d_model)
+        # (B, N, H, dk) memory, viewed as (B, H, N, dk): no transpose copies on the GPU path
+        with annotate("qkv_proj"):
+            q = self.q_proj(x3).view(B, N, H, dk).transpose(1, 2)
+            k = self.k_proj(x3).view(B, N, H, dk).transpose(1, 2)
+            v = self.v_proj(x3).view(B, N, H, dk).transpose(1, 2)
+        pos = token_positions
+        if pos is not None:
+            pos = pos.reshape(-1, N) if pos.numel() != N else pos.reshape(N)
+        with annotate("rope"):
+            q = self.positional_encoder(q, pos)
+            k = self.positional_encoder(k, pos)
+        impl = _ATTN_IMPL
+        with annotate("attention"):
+            if impl == "naive" or (impl == "auto" and not x.is_cuda):
+                seq = torch.arange(N, device=x.device)
+                mask = seq[:, None] >= seq[None, :]
+                o = scaled_dot_product_attention(q, k, v, mask)
+            elif x.is_cuda:
+                o = ops.flash_attention(q, k.to(q.dtype), v.to(q.dtype), is_causal=True)
+            else:
+                o = ops.FlashAttentionTorch.apply(q, k, v, True)
+        o = o.transpose(1, 2).reshape(*b, N, H * dk) if b else o.transpose(1, 2).reshape(N, H * dk)
+        with annotate("out_proj"):
+            return self.output_proj(o)
+
+
+class TransformerBlock(nn.Module):
+    """Pre-norm block: ``x + attn(ln1(x))`` then ``+ ffn(ln2(.))`` (``model.py:330-386``)."""
+
+    def __init__(self, d_model: int, num_heads: int, d_ff: int, positional_encoder: RotaryEmbedding, device=None, dtype=None):
+        super().__init__()
+        self.attn = CausalMultiHeadSelfAttention(d_model, num_heads, positional_encoder, device, dtype)
+        self.ffn = SwiGLU(d_model, d_ff, device, dtype)
+        self.ln1 = RMSNorm(d_model, device=device, dtype=dtype)
+        self.ln2 = RMSNorm(d_model, device=device, dtype=dtype)
+
+    def forward(self, x: torch.Tensor, token_positions: torch.Tensor | None = None):
+        with annotate("block.attn"):
+            h = x + self.attn(self.ln1(x), token_positions)
+        with annotate("block.ffn"):
+            return h + self.ffn(self.ln2(h))
+
+
+class BasicsTransformerLM(nn.Module):
+    """Transformer LM with the reference constructor (``model.py:153-191``).
+
+    ``self.config`` holds exactly the constructor kwargs (serialized to ``model_config.json``).
+    """
+
+    def __init__(
+        self,
+        vocab_size: int,
+        context_length: int,
+        d_model: int,
+        num_layers: int,
+        num_heads: int,
+        d_ff: int,
+        rope_theta: float = 10000.0,
+        *,
+        device=None,
+        dtype=None,
+    ):
+        self.config = dict(
+            vocab_size=vocab_size,
+            context_length=context_length,
+            d_model=d_model,
+            num_layers=num_layers,
+            num_heads=num_heads,
+            d_ff=d_ff,
+            rope_theta=rope_theta,
+        )
+        super().__init__()
+        self.vocab_size = vocab_size
+        self.context_length = context_length
+        self.d_model = d_model
+        self.token_embeddings = Embedding(vocab_size, d_model, device, dtype)
+        self.positional_encoder = RotaryEmbedding(context_length, d_model // num_heads, rope_theta, device)
+        self.layers = nn.ModuleList(
+            [TransformerBlock(d_model, num_heads, d_ff, self.positional_encoder, device, dtype) for _ in range(num_layers)]
+        )
+        self.ln_final = RMSNorm(d_model, device=device, dtype=dtype)
+        self.lm_head = Linear(d_model, vocab_size, device, dtype)
+        logger.info(f"number of non-embedding parameters: {self.get_num_params() / 1e6:.2f}M")
+
+    def get_num_params(self, non_embedding: bool = True) -> int:
+        n = sum(p.numel() for p in self.parameters())
+        if non_embedding:
+            n -= self.lm_head.weight.numel()
+        return n
+
+    def forward(self, x: torch.Tensor, token_positions: torch.Tensor | None = None) -> torch.Tensor:
+        with annotate("embed"):
+            h = self.token_embeddings(x)
+        for i, layer in enumerate(self.layers):
+            with annotate(f"layer{i}"):
+                h = layer(h, token_positions)
+        with annotate("lm_head"):
+            return self.lm_head(self.ln_final(h))
+
+    @torch.no_grad()
+    def generate(
+        self,
+        x: torch.Tensor,
+        max_new_tokens: int,
+        temperature: float = 1.0,
+        top_k: int | None = None,
+        eos_token_id: int | None = None,
+    ) -> torch.Tensor:
+        """Autoregressive sampling (``model.py:255-310``) with a working top-k filter (the
+        reference's ``masked_fill`` is not in place and its threshold broadcast is wrong for B>1)."""
+        if x.dim() == 1:
+            x = x.unsqueeze(0)
+        orig = x.size(-1)
+        for _ in range(max_new_tokens):
+            ctx = x[:, -self.context_length :] if x.size(1) > self.context_length else x
+            logits = self.forward(ctx)[:, -1].float() / temperature
+            if top_k:
+                vals, _ = torch.topk(logits, min(top_k, logits.size(-1)))
+                logits = logits.masked_fill(logits < vals[:, -1:], float("-inf"))
+            probs = softmax(logits, dim=-1)
+            nxt = torch.multinomial(probs, 1)
+            if eos_token_id is not None and x.size(0) == 1 and nxt.item() == eos_token_id:
+                break
+            x = torch.cat((x, nxt), dim=-1)
+        return x[:, orig:]
+
+    @classmethod
+    def from_pretrained(cls, pretrained_model_path: str, map_location=None):
+        with open(os.path.join(pretrained_model_path, "model_config.json")) as f:
+            config = json.load(f)
+        model = cls(**config)
+        state_dict = torch.load(os.path.join(pretrained_model_path, "model.pt"), map_location=map_location, weights_only=True)
+        prefix = "_orig_mod."
+        for k in list(state_dict.keys()):
+            if k.startswith(prefix):
+                state_dict[k[len(prefix) :]] = state_dict.pop(k)
+        model.load_state_dict(state_dict)
+        return model
+
+    def save_pretrained(self, path: str) -> None:
+        os.makedirs(path, exist_ok=True)
+        with open(os.path.join(path, "model_config.json"), "w") as f:
+            json.dump(self.config, f, indent=2)
+        torch.save(self.state_dict(), os.path.join(path, "model.pt"))

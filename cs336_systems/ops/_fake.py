@@ -1,0 +1,64 @@
+"""Fake (meta) implementations of the ``torch.ops.cs336`` kernels so that ``torch.compile`` and
+FakeTensor tracing see correct output shapes/dtypes/strides without running HIP code."""
+
+from __future__ import annotations
+
+import torch
+from torch.library import register_fake
+
+
+def _bnhd_like(q):
+    B, H, N, D = q.shape
+    return q.new_empty((B, N, H, D)).permute(0, 2, 1, 3)
+
+
+@register_fake("cs336::fa_fwd")
+def _fa_fwd(q, k, v, causal, scale):
+    B, H, N, D = q.shape
+    return _bnhd_like(q), q.new_empty((B, H, N), dtype=torch.float32)
+
+
+@register_fake("cs336::fa_bwd")
+def _fa_bwd(do, q, k, v, o, lse, causal, scale):
+    return _bnhd_like(q), _bnhd_like(k), _bnhd_like(v)
+
+
+@register_fake("cs336::rmsnorm_fwd")
+def _rms_fwd(x, w, eps, out_dtype):
+    return x.new_empty(x.shape, dtype=out_dtype or x.dtype), x.new_empty((x.shape[0],), dtype=torch.float32)
+
+
+@register_fake("cs336::rmsnorm_bwd")
+def _rms_bwd(dy, x, w, rstd):
+    return torch.empty_like(x), w.new_empty(w.shape, dtype=torch.float32)
+
+
+@register_fake("cs336::rope")
+def _rope(x, cos, sin, pos, inverse):
+    return _bnhd_like(x)
+
+
+@register_fake("cs336::silu_mul_fwd")
+def _sm_fwd(a, b):
+    return torch.empty_like(a)
+
+
+@register_fake("cs336::silu_mul_bwd")
+def _sm_bwd(dh, a, b):
+    return torch.empty_like(a), torch.empty_like(b)
+
+
+@register_fake("cs336::xent_fwd")
+def _xent_fwd(z, t):
+    M = z.shape[0]
+    return z.new_empty((M,), dtype=torch.float32), z.new_empty((M,), dtype=torch.float32)
+
+
+@register_fake("cs336::xent_bwd")
+def _xent_bwd(g, z, t, lse, mult):
+    return torch.empty_like(z)
+
+
+@register_fake("cs336::multi_tensor_l2norm")
+def _l2(ts):
+    return ts[0].new_empty((), dtype=torch.float32)

@@ -1,0 +1,126 @@
+"""Fused multi-tensor AdamW (``csrc/ops/adamw.hip``) with the exact update order of the cs336
+AdamW (``cs336-basics/cs336_basics/optimizer.py:50-86``):
+
+    m = b1*m + (1-b1)*g ;  v = b2*v + (1-b2)*g^2
+    alpha_t = lr * sqrt(1-b2^t) / (1-b1^t)
+    p -= alpha_t * m / (sqrt(v) + eps)
+    p -= lr * wd * p                      # decoupled decay, applied to the *updated* p
+
+The reference runs ~9 eager kernels per parameter tensor from a Python loop (80-120 ms per step
+for 3.4 B params on H100). Here the whole model is one launch per (dtype, step)
+group: a chunk table (tensor pointer, chunk offset) is built on the host and every workgroup
+streams one 16 KiB-per-wave chunk with 16-byte vector loads, so the step is HBM-bound
+(28 B/param: read p,g,m,v; write p,m,v).
+"""
+
+from __future__ import annotations
+
+import math
+from collections.abc import Callable, Iterable
+
+import torch
+
+from ._ext import ops, use_hip
+
+
+def adamw_ref_(p, g, m, v, lr, beta1, beta2, eps, wd, t):
+    """In-place reference update for one tensor (fp32 math)."""
+    m.mul_(beta1).add_(g, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    alpha_t = lr * math.sqrt(1 - beta2**t) / (1 - beta1**t)
+    p.sub_(alpha_t * m / (torch.sqrt(v) + eps))
+    p.sub_(lr * wd * p)
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """Drop-in for ``cs336_basics.optimizer.AdamW`` that runs one HIP launch per step.
+
+    State per parameter: ``m``, ``v`` (same dtype as the parameter) and ``t`` (next step index,
+    starting at 1), identical to the reference so state dicts interchange.
+    """
+
+    def __init__(
+        self,
+        params: Iterable[torch.nn.Parameter],
+        lr: float = 1e-3,
+        betas: tuple[float, float] = (0.9, 0.999),
+        eps: float = 1e-8,
+        weight_decay: float = 0.01,
+    ):
+        if not 0.0 <= lr:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= eps:
+            raise ValueError(f"Invalid epsilon value: {eps}")
+        if not 0.0 <= betas[0] < 1.0:
+            raise ValueError(f"Invalid beta parameter at index 0: {betas[0]}")
+        if not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"Invalid beta parameter at index 1: {betas[1]}")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self, closure: Callable | None = None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            lr = group["lr"]
+            beta1, beta2 = group["betas"]
+            eps = group["eps"]
+            wd = group["weight_decay"]
+            # bucket by (device, dtype, t) so each launch has a single bias correction
+            buckets: dict[tuple, tuple[list, list, list, list]] = {}
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("AdamW does not support sparse gradients")
+                state = self.state[p]
+                if "m" not in state:
+                    state["m"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    state["v"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    state["t"] = 1
+                key = (p.device, p.dtype, p.grad.dtype, state["t"])
+                b = buckets.setdefault(key, ([], [], [], []))
+                b[0].append(p)
+                b[1].append(p.grad)
+                b[2].append(state["m"])
+                b[3].append(state["v"])
+                state["t"] += 1
+            for (dev, _, _, t), (ps, gs, ms, vs) in buckets.items():
+                if use_hip(ps[0]) and all(x.is_contiguous() for x in ps + gs + ms + vs):
+                    ops().adamw_step(ps, gs, ms, vs, lr, beta1, beta2, eps, wd, t)
+                else:
+                    for p, g, m, v in zip(ps, gs, ms, vs):
+                        adamw_ref_(p, g.to(p.dtype), m, v, lr, beta1, beta2, eps, wd, t)
+        return loss
+
+
+def multi_tensor_l2norm(tensors: list[torch.Tensor]) -> torch.Tensor:
+    """Global L2 norm over a list of tensors as a 0-d fp32 device tensor (no host sync)."""
+    tensors = [t for t in tensors if t is not None and t.numel() > 0]
+    if not tensors:
+        return torch.zeros(())
+    if use_hip(tensors[0]) and all(t.is_contiguous() for t in tensors):
+        return ops().multi_tensor_l2norm(tensors)
+    total = torch.zeros((), dtype=torch.float32, device=tensors[0].device)
+    for t in tensors:
+        total = total + t.float().pow(2).sum()
+    return total.sqrt()
+
+
+def clip_grad_norm_(parameters: Iterable[torch.nn.Parameter], max_norm: float) -> torch.Tensor:
+    """Global-norm clip with the cs336 rule ``g *= min(1, max_norm / (norm + 1e-6))``
+    (``cs336-basics/cs336_basics/nn_utils.py:20-30``) fully on device: one multi-tensor norm
+    kernel + one multi-tensor scale kernel, no ``.item()``."""
+    grads = [p.grad for p in parameters if p.grad is not None]
+    if not grads:
+        return torch.zeros(())
+    norm = multi_tensor_l2norm(grads)
+    coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+    if use_hip(grads[0]) and all(g.is_contiguous() for g in grads):
+        ops().multi_tensor_scale_(grads, coef)
+    else:
+        for g in grads:
+            g.mul_(coef.to(g.dtype))
+    return norm

@@ -1,0 +1,48 @@
+from .comm import (
+    broadcast_module_,
+    cleanup_distributed,
+    default_backend,
+    find_free_port,
+    setup_distributed,
+    spawn,
+    supports_avg,
+)
+from .ddp import DDP, DDP_Bucketed, DDPBucketed, DDPIndividual, DEFAULT_BUCKET_MB, FlatDDP, NaiveDDP
+from .sharded_optimizer import ShardedOptimizer, ShardedStateOptimizer
+
+DDP_VARIANTS = {
+    "naive": NaiveDDP,
+    "flat": FlatDDP,
+    "individual": DDPIndividual,
+    "bucketed": DDPBucketed,
+}
+
+
+def wrap_ddp(module, variant: str = "bucketed", bucket_size_mb: float | None = DEFAULT_BUCKET_MB, **kw):
+    """Wrap ``module`` with one of the four DP variants by name."""
+    cls = DDP_VARIANTS[variant]
+    if cls is DDPBucketed:
+        return cls(module, bucket_size_mb=bucket_size_mb, **kw)
+    return cls(module, **kw)
+
+
+__all__ = [
+    "DDP",
+    "DDP_Bucketed",
+    "DDPBucketed",
+    "DDPIndividual",
+    "DDP_VARIANTS",
+    "DEFAULT_BUCKET_MB",
+    "FlatDDP",
+    "NaiveDDP",
+    "ShardedOptimizer",
+    "ShardedStateOptimizer",
+    "broadcast_module_",
+    "cleanup_distributed",
+    "default_backend",
+    "find_free_port",
+    "setup_distributed",
+    "spawn",
+    "supports_avg",
+    "wrap_ddp",
+]

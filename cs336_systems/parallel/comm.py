@@ -1,0 +1,119 @@
+"""Process-group setup and small collective helpers (RCCL on GPU, Gloo on CPU).
+
+Reference parity: ``naive_ddp.py:35-51``, ``ddp_bucketed_overlapped_sharded.py:46-49``,
+``distributed_communication_single.py:11-26`` and ``tests/common.py:71-94`` each hand-roll an
+env:// rendezvous on localhost with ``mp.spawn``. Here one helper serves both launch styles:
+
+* ``torchrun`` / ``python -m torch.distributed.run`` (``RANK``/``LOCAL_RANK``/``WORLD_SIZE`` in the
+  env) — the way ``bench.py`` and the scaling runs are launched: one process per MI355X;
+* ``mp.spawn`` for tests and small drivers (:func:`spawn`, picks a free port on 127.0.0.1).
+
+On ROCm the ``"nccl"`` backend *is* RCCL (xGMI peer-to-peer between the 8 GPUs of a node).
+"""
+
+from __future__ import annotations
+
+import datetime
+import os
+import socket
+from collections.abc import Callable
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def find_free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def default_backend(device: str | torch.device | None = None) -> str:
+    if device is not None:
+        return "nccl" if torch.device(device).type == "cuda" else "gloo"
+    return "nccl" if torch.cuda.is_available() else "gloo"
+
+
+def setup_distributed(
+    rank: int | None = None,
+    world_size: int | None = None,
+    backend: str | None = None,
+    master_addr: str | None = None,
+    master_port: int | str | None = None,
+    timeout_s: float = 600.0,
+) -> tuple[int, int, torch.device]:
+    """Initialise the default process group; returns ``(rank, world_size, device)``.
+
+    Missing arguments come from the torchrun environment. Binds the process to GPU
+    ``LOCAL_RANK % device_count`` before init so RCCL picks the right device.
+    """
+    rank = int(os.environ.get("RANK", 0)) if rank is None else rank
+    world_size = int(os.environ.get("WORLD_SIZE", 1)) if world_size is None else world_size
+    local_rank = int(os.environ.get("LOCAL_RANK", rank))
+    os.environ["MASTER_ADDR"] = master_addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(master_port or os.environ.get("MASTER_PORT", "29512"))
+    # async error handling: a hung/failed peer raises instead of deadlocking
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    if backend is None:
+        backend = default_backend()
+    if backend == "nccl" and torch.cuda.is_available():
+        dev = torch.device("cuda", local_rank % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    if not dist.is_initialized():
+        kw = {}
+        if backend == "nccl" and dev.type == "cuda":
+            kw["device_id"] = dev
+        dist.init_process_group(
+            backend, rank=rank, world_size=world_size, timeout=datetime.timedelta(seconds=timeout_s), **kw
+        )
+    return rank, world_size, dev
+
+
+def cleanup_distributed() -> None:
+    if dist.is_initialized():
+        try:
+            dist.barrier()
+        finally:
+            dist.destroy_process_group()
+
+
+def spawn(fn: Callable, world_size: int, *args, port: int | None = None) -> None:
+    """``mp.spawn`` ``fn(rank, world_size, *args)`` with a fresh 127.0.0.1 rendezvous port."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port or find_free_port())
+    mp.spawn(fn, args=(world_size, *args), nprocs=world_size, join=True)
+
+
+def supports_avg(group=None) -> bool:
+    """RCCL/NCCL implement ReduceOp.AVG natively (saves the separate divide kernel); Gloo does not."""
+    return dist.get_backend(group) == "nccl"
+
+
+def broadcast_module_(module: torch.nn.Module, src: int = 0, group=None, buffer_mb: int = 256) -> None:
+    """Broadcast every parameter of ``module`` from ``src`` with coalesced collectives (a few
+    large RCCL broadcasts instead of one per tensor, reference ``:225-226``)."""
+    params = [p.data for p in module.parameters()]
+    if not params:
+        return
+    if group is None:
+        group = dist.group.WORLD
+    dist._broadcast_coalesced(group, params, buffer_mb * 1024 * 1024, src)
+
+
+def all_reduce_mean_scalar(x: float, device) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(t, op=dist.ReduceOp.AVG)
+    else:
+        dist.all_reduce(t)
+        t /= dist.get_world_size()
+    return float(t.item())
+
+
+def all_reduce_max_scalar(x: float, device) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -1,0 +1,266 @@
+"""Data-parallel gradient synchronization, four variants.
+
+=====================  ==================================================  ==========================
+class                  mechanism                                           reference
+=====================  ==================================================  ==========================
+``NaiveDDP``           blocking all-reduce per parameter after backward   ``naive_ddp.py:173-267``
+``FlatDDP``            one blocking all-reduce of a persistent flat grad   ``naive_ddp.py:444-634``
+                       buffer (grads are views into it, no flatten copy)
+``DDPIndividual``      async all-reduce per parameter from its post-        ``ddp_bucketed_overlapped_
+                       accumulate-grad hook, overlapped with backward       sharded.py:217-248``
+``DDPBucketed``        async all-reduce per bucket, overlapped with         ``…:251-318``
+                       backward; buckets are persistent flat buffers and
+                       ``param.grad`` is a *view* into them (zero-copy)
+=====================  ==================================================  ==========================
+
+MI355X/RCCL design notes:
+
+* RCCL collectives run on the process group's own HIP stream; ProcessGroupNCCL records an event on
+  the current (compute) stream before each launch, so an all-reduce issued from a grad hook runs
+  concurrently with the rest of backward and ``Work.wait()`` only inserts a stream dependency (the
+  host never blocks).
+* With the nccl(=RCCL) backend the mean is taken by ``ReduceOp.AVG`` inside the collective; Gloo
+  (CPU tests) uses SUM followed by one in-place divide per flat bucket.
+* Bucket cap: xGMI is 7 point-to-point links per GPU (~153 GB/s each); RCCL only reaches its
+  multi-channel bus bandwidth with messages of tens of MB, while the last bucket's all-reduce is
+  exposed after backward. The default cap (``DEFAULT_BUCKET_MB``) balances those two; see
+  ``cs336_systems/bench/collectives.py`` for the size sweep that backs it.
+* Unlike the reference, buckets hold only ``requires_grad`` parameters (no empty bucket 0, frozen
+  params never block a flush) and a bucket whose parameters received no gradient on this rank is
+  still reduced at ``finish_gradient_synchronization`` (zeros), so ranks never deadlock.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..utils.profiling import annotate
+from .comm import broadcast_module_, supports_avg
+
+DEFAULT_BUCKET_MB = 128.0
+
+
+def _unique_params(module: nn.Module) -> list[nn.Parameter]:
+    return list(module.parameters())  # parameters() already de-duplicates tied weights
+
+
+class _DDPBase(nn.Module):
+    def __init__(self, module: nn.Module, process_group=None, broadcast: bool = True):
+        super().__init__()
+        self.module = module
+        self.process_group = process_group
+        self.world_size = dist.get_world_size(process_group)
+        self.rank = dist.get_rank(process_group)
+        self._avg = supports_avg(process_group)
+        if broadcast:
+            broadcast_module_(module, src=0, group=process_group)
+
+    def forward(self, *inputs, **kwargs):
+        return self.module(*inputs, **kwargs)
+
+    def _all_reduce(self, t: torch.Tensor, async_op: bool):
+        op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
+        return dist.all_reduce(t, op=op, group=self.process_group, async_op=async_op)
+
+    def _finish_mean(self, t: torch.Tensor) -> None:
+        if not self._avg and self.world_size > 1:
+            t.div_(self.world_size)
+
+    def finish_gradient_synchronization(self) -> None:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+
+class NaiveDDP(_DDPBase):
+    """Synchronous per-parameter all-reduce after backward (the handout's naive baseline)."""
+
+    def finish_gradient_synchronization(self) -> None:
+        for p in _unique_params(self.module):
+            if p.requires_grad and p.grad is not None:
+                self._all_reduce(p.grad, async_op=False)
+                self._finish_mean(p.grad)
+
+
+class FlatDDP(_DDPBase):
+    """One blocking all-reduce over a persistent flat gradient buffer.
+
+    ``param.grad`` tensors are views into ``self.flat`` (re-attached after ``zero_grad(set_to_none=
+    True)``), so there is no flatten/unflatten copy (reference ``naive_ddp.py:543-553`` copies twice).
+    """
+
+    def __init__(self, module: nn.Module, process_group=None, broadcast: bool = True):
+        super().__init__(module, process_group, broadcast)
+        self._params = [p for p in _unique_params(module) if p.requires_grad]
+        self._groups: dict[tuple, tuple[torch.Tensor, list]] = {}
+        by_key: dict[tuple, list] = {}
+        for p in self._params:
+            by_key.setdefault((p.device, p.dtype), []).append(p)
+        self._views = {}
+        for key, ps in by_key.items():
+            flat = torch.zeros(sum(p.numel() for p in ps), device=key[0], dtype=key[1])
+            off = 0
+            for p in ps:
+                self._views[p] = flat[off : off + p.numel()].view_as(p)
+                off += p.numel()
+            self._groups[key] = (flat, ps)
+        self.zero_grad()
+
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        for flat, ps in self._groups.values():
+            flat.zero_()
+            for p in ps:
+                p.grad = self._views[p]
+
+    def finish_gradient_synchronization(self) -> None:
+        for flat, ps in self._groups.values():
+            for p in ps:
+                v = self._views[p]
+                if p.grad is None:
+                    v.zero_()
+                elif p.grad.data_ptr() != v.data_ptr():
+                    v.copy_(p.grad)
+                p.grad = v
+            with annotate("flat_allreduce"):
+                self._all_reduce(flat, async_op=False)
+            self._finish_mean(flat)
+
+
+class DDPIndividual(_DDPBase):
+    """Overlapped per-parameter all-reduce issued from post-accumulate-grad hooks."""
+
+    def __init__(self, module: nn.Module, process_group=None, broadcast: bool = True):
+        super().__init__(module, process_group, broadcast)
+        self._handles: list[tuple[object, torch.Tensor]] = []
+        self._hooks = []
+        for p in _unique_params(module):
+            if p.requires_grad:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
+
+    def _on_grad_ready(self, p: torch.Tensor) -> None:
+        with annotate("comm.param"):
+            self._handles.append((self._all_reduce(p.grad, async_op=True), p.grad))
+
+    def finish_gradient_synchronization(self) -> None:
+        for h, g in self._handles:
+            h.wait()
+            self._finish_mean(g)
+        self._handles.clear()
+
+
+class _Bucket:
+    __slots__ = ("idx", "params", "flat", "pending", "handle", "launched")
+
+    def __init__(self, idx: int, params: list, flat: torch.Tensor):
+        self.idx = idx
+        self.params = params
+        self.flat = flat
+        self.pending = len(params)
+        self.handle = None
+        self.launched = False
+
+
+class DDPBucketed(_DDPBase):
+    """Overlapped bucketed all-reduce with persistent, zero-copy bucket buffers.
+
+    Buckets are filled greedily over ``reversed(module.parameters())`` (≈ the order in which
+    backward produces gradients) up to ``bucket_size_mb`` (``None`` → one unbounded bucket);
+    a bucket never mixes dtypes/devices. Each parameter's ``.grad`` is a view into its bucket's
+    flat buffer, so autograd accumulates straight into the communication buffer. If a caller
+    resets grads to ``None`` (``optimizer.zero_grad()``), the hook copies the fresh gradient into
+    the view once and re-attaches it; calling :meth:`zero_grad` (or
+    ``on_train_batch_start``) instead keeps the zero-copy path.
+    """
+
+    def __init__(self, module: nn.Module, bucket_size_mb: float | None = DEFAULT_BUCKET_MB, process_group=None, broadcast: bool = True):
+        super().__init__(module, process_group, broadcast)
+        self.bucket_size_mb = bucket_size_mb
+        cap = float("inf") if bucket_size_mb is None else bucket_size_mb * 1024 * 1024
+        params = [p for p in _unique_params(module) if p.requires_grad]
+        groups: list[list[nn.Parameter]] = []
+        cur: list[nn.Parameter] = []
+        cur_bytes = 0
+        for p in reversed(params):
+            nbytes = p.numel() * p.element_size()
+            if cur and (cur_bytes + nbytes > cap or p.dtype != cur[0].dtype or p.device != cur[0].device):
+                groups.append(cur)
+                cur, cur_bytes = [], 0
+            cur.append(p)
+            cur_bytes += nbytes
+        if cur:
+            groups.append(cur)
+        self.buckets: list[_Bucket] = []
+        self._param_bucket: dict[nn.Parameter, _Bucket] = {}
+        self._views: dict[nn.Parameter, torch.Tensor] = {}
+        for i, ps in enumerate(groups):
+            flat = torch.zeros(sum(p.numel() for p in ps), device=ps[0].device, dtype=ps[0].dtype)
+            off = 0
+            for p in ps:
+                self._views[p] = flat[off : off + p.numel()].view_as(p)
+                self._param_bucket[p] = None  # filled below
+                off += p.numel()
+            b = _Bucket(i, ps, flat)
+            self.buckets.append(b)
+            for p in ps:
+                self._param_bucket[p] = b
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in params]
+        self.zero_grad()
+
+    # ---- grad buffer management -------------------------------------------------------------
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        """Zero every bucket (one memset per bucket) and point each ``.grad`` at its view."""
+        for b in self.buckets:
+            b.flat.zero_()
+            for p in b.params:
+                p.grad = self._views[p]
+
+    def on_train_batch_start(self) -> None:
+        self.zero_grad()
+
+    def _adopt(self, p: nn.Parameter) -> None:
+        v = self._views[p]
+        g = p.grad
+        if g is None:
+            v.zero_()
+        elif g.data_ptr() != v.data_ptr():
+            v.copy_(g)
+        p.grad = v
+
+    # ---- hooks ------------------------------------------------------------------------------
+    def _launch(self, b: _Bucket) -> None:
+        with annotate(f"comm.bucket{b.idx}"):
+            b.handle = self._all_reduce(b.flat, async_op=True)
+        b.launched = True
+
+    def _on_grad_ready(self, p: nn.Parameter) -> None:
+        b = self._param_bucket[p]
+        self._adopt(p)
+        b.pending -= 1
+        if b.pending == 0 and not b.launched:
+            self._launch(b)
+
+    def finish_gradient_synchronization(self) -> None:
+        # buckets with parameters that got no gradient on this rank are reduced now, in the same
+        # order on every rank (by bucket index)
+        for b in self.buckets:
+            if not b.launched:
+                for p in b.params:
+                    self._adopt(p)
+                self._launch(b)
+        for b in self.buckets:
+            b.handle.wait()
+            self._finish_mean(b.flat)
+            b.handle = None
+            b.launched = False
+            b.pending = len(b.params)
+
+    def bucket_summary(self) -> list[dict]:
+        return [
+            dict(bucket=b.idx, n_params=len(b.params), mb=b.flat.numel() * b.flat.element_size() / 2**20)
+            for b in self.buckets
+        ]
+
+
+# Reference class names (``ddp_bucketed_overlapped_sharded.py``) for drop-in users.
+DDP = DDPIndividual
+DDP_Bucketed = DDPBucketed

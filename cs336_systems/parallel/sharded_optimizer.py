@@ -1,0 +1,155 @@
+"""ZeRO-1-style optimizer-state sharding (reference
+``ddp_bucketed_overlapped_sharded.py:322-362``).
+
+Semantics kept from the reference:
+
+* wraps *any* ``optimizer_cls``; each parameter is owned by exactly one rank, chosen greedily as
+  the rank with the fewest owned bytes so far (``argmin``), in parameter order;
+* each rank runs the unmodified ``optimizer_cls`` on its own parameters only, so optimizer state
+  is ~1/W per rank and results are bit-identical to the unsharded optimizer
+  (``tests/test_sharded_optimizer.py`` checks rtol=1e-7).
+
+MI355X-first changes:
+
+* after the local step, updated parameters are shipped with **one all-gather per dtype**
+  (``all_gather_into_tensor`` of each rank's packed shard, padded to the largest shard) plus a
+  single multi-tensor copy to unpack, instead of one broadcast per parameter (291-435 RCCL
+  launches per step for the 2.7b/XL models in the reference). Packing/unpacking are pure copies,
+  so values stay exact;
+* a rank that owns no parameters still participates (the reference crashed on ``None``);
+* hyper-parameter edits on ``self.param_groups`` (LR schedules) are forwarded to the local
+  optimizer every step.
+"""
+
+from __future__ import annotations
+
+from collections.abc import Callable
+from typing import Any
+
+import torch
+import torch.distributed as dist
+
+
+class ShardedOptimizer(torch.optim.Optimizer):
+    def __init__(self, params, optimizer_cls: type[torch.optim.Optimizer], process_group=None, **kwargs: Any):
+        self.optimizer_cls = optimizer_cls
+        self.kwargs = kwargs
+        self.process_group = process_group
+        self.rank = dist.get_rank(process_group)
+        self.world_size = dist.get_world_size(process_group)
+        self.optimizer: torch.optim.Optimizer | None = None
+        self.param_to_rank: dict[int, int] = {}
+        self.rank_sizes = [0] * self.world_size
+        self._local_group_of: dict[int, int] = {}  # global group idx -> local group idx
+        self._sync_plan = None
+        super().__init__(params, defaults=dict(kwargs))
+
+    # ------------------------------------------------------------------------------------------
+    def add_param_group(self, param_group: dict[str, Any]) -> None:
+        super().add_param_group(param_group)
+        g = self.param_groups[-1]
+        gidx = len(self.param_groups) - 1
+        local = []
+        for p in g["params"]:
+            owner = min(range(self.world_size), key=lambda r: (self.rank_sizes[r], r))
+            self.param_to_rank[id(p)] = owner
+            self.rank_sizes[owner] += p.numel() * p.element_size()
+            if owner == self.rank:
+                local.append(p)
+        if local:
+            cfg = {k: v for k, v in g.items() if k != "params"}
+            lg = {"params": local, **cfg}
+            if self.optimizer is None:
+                self.optimizer = self.optimizer_cls([lg], **self.kwargs)
+            else:
+                self.optimizer.add_param_group(lg)
+            self._local_group_of[gidx] = len(self.optimizer.param_groups) - 1
+        self._sync_plan = None
+
+    def owner_of(self, p: torch.Tensor) -> int:
+        return self.param_to_rank[id(p)]
+
+    # ------------------------------------------------------------------------------------------
+    def _forward_hparams(self) -> None:
+        if self.optimizer is None:
+            return
+        for gi, li in self._local_group_of.items():
+            src, dst = self.param_groups[gi], self.optimizer.param_groups[li]
+            for k, v in src.items():
+                if k != "params":
+                    dst[k] = v
+
+    @torch.no_grad()
+    def step(self, closure: Callable | None = None, **kwargs):
+        self._forward_hparams()
+        loss = None
+        if self.optimizer is not None:
+            loss = self.optimizer.step(closure, **kwargs)
+        elif closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self.sync_parameters()
+        return loss
+
+    # ------------------------------------------------------------------------------------------
+    def _build_plan(self):
+        """Per (device, dtype): params of every rank in global order, shard sizes, buffers."""
+        plan = {}
+        for g in self.param_groups:
+            for p in g["params"]:
+                key = (p.device, p.dtype)
+                plan.setdefault(key, [[] for _ in range(self.world_size)])[self.param_to_rank[id(p)]].append(p)
+        out = []
+        for (dev, dtype), per_rank in plan.items():
+            sizes = [sum(p.numel() for p in ps) for ps in per_rank]
+            smax = max(sizes) if sizes else 0
+            if smax == 0:
+                continue
+            send = torch.empty(smax, device=dev, dtype=dtype)
+            recv = torch.empty(smax * self.world_size, device=dev, dtype=dtype)
+            out.append((per_rank, sizes, smax, send, recv))
+        self._sync_plan = out
+
+    @torch.no_grad()
+    def sync_parameters(self) -> None:
+        """All-gather every rank's updated shard and copy the values into the replicas."""
+        if self.world_size == 1:
+            return
+        if self._sync_plan is None:
+            self._build_plan()
+        for per_rank, sizes, smax, send, recv in self._sync_plan:
+            mine = per_rank[self.rank]
+            if mine:
+                torch.cat([p.detach().reshape(-1) for p in mine], out=send[: sizes[self.rank]])
+            dist.all_gather_into_tensor(recv, send, group=self.process_group)
+            dst, src = [], []
+            for r in range(self.world_size):
+                if r == self.rank or not per_rank[r]:
+                    continue
+                off = r * smax
+                for p in per_rank[r]:
+                    n = p.numel()
+                    dst.append(p.data)
+                    src.append(recv[off : off + n].view_as(p))
+                    off += n
+            if dst:
+                torch._foreach_copy_(dst, src)
+
+    # ------------------------------------------------------------------------------------------
+    def state_dict(self):
+        """Local shard state (plus ownership), like the reference; see :meth:`consolidated_state_dict`."""
+        return {
+            "local": self.optimizer.state_dict() if self.optimizer is not None else None,
+            "rank": self.rank,
+            "world_size": self.world_size,
+        }
+
+    def load_state_dict(self, state_dict):
+        if state_dict["world_size"] != self.world_size or state_dict["rank"] != self.rank:
+            raise ValueError("sharded optimizer state must be loaded with the same world size/rank")
+        if self.optimizer is not None and state_dict["local"] is not None:
+            self.optimizer.load_state_dict(state_dict["local"])
+
+
+# reference name
+ShardedStateOptimizer = ShardedOptimizer
