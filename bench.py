@@ -1,0 +1,203 @@
+#!/usr/bin/env python
+"""Headline benchmark: GPT-2-XL-shape Transformer LM, bf16 mixed-precision full training step,
+data-parallel over RCCL/xGMI, tokens/s for the whole node (BASELINE.json metric/config).
+
+    python bench.py --gpus 1 --steps 10 --warmup 3
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 10 --warmup 3
+
+One step = zero grads → forward (bf16 autocast over fp32 master weights; HIP RMSNorm/RoPE/
+FlashAttention-2/SwiGLU kernels, hipBLASLt GEMMs) → fused HIP cross-entropy → backward with the
+bucketed DDP all-reduce overlapped (N > 1) → fused multi-tensor HIP AdamW on all 2.0 B params.
+Model "xl" = d_model 1600, 48 layers, 25 heads (d_head 64), d_ff 6400, vocab 10000, ctx 512
+(reference ``cs336_systems/benchmark.py:247-259``), random init, synthetic tokens.
+Weak scaling: the per-GPU batch is fixed, so global batch = batch * N.
+Timing: W untimed warmup steps, then barrier + synchronize, K steps, synchronize + barrier;
+the slowest rank's wall time is reported (MAX over ranks).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "tokens/sec/node GPT-2-XL bf16 DDP"
+BASELINE_VALUE = None  # the reference publishes no number
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="xl")
+    ap.add_argument("--ctx", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("CS336_BENCH_BATCH", 16)), help="per-GPU batch")
+    ap.add_argument("--vocab", type=int, default=10000)
+    ap.add_argument("--ddp", default="bucketed", choices=["bucketed", "individual", "flat", "naive"])
+    ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--sharded", action="store_true", help="ZeRO-1 sharded optimizer state")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--clip", type=float, default=0.0, help="global grad-norm clip (0 = off, as the reference bench)")
+    ap.add_argument("--backend", default=os.environ.get("CS336_BACKEND", "auto"))
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    rank = int(os.environ.get("RANK", "0"))
+
+    from cs336_systems import ops
+    from cs336_systems.data import synthetic_batch
+    from cs336_systems.models import build_model, get_model_config, param_count, train_flops_per_token
+    from cs336_systems.parallel import DEFAULT_BUCKET_MB, ShardedOptimizer, setup_distributed, wrap_ddp
+
+    ops.set_backend(args.backend)
+    if world > 1:
+        rank, world, device = setup_distributed(backend="nccl")
+    else:
+        device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        if device.type == "cuda":
+            torch.cuda.set_device(device)
+    if device.type == "cuda":
+        assert ops.ext_available(), ops.load_error()
+        torch.backends.cuda.matmul.allow_tf32 = False
+
+    torch.manual_seed(1234)
+    t0 = time.time()
+    model = build_model(args.model, args.ctx, vocab_size=args.vocab, device=device)
+    n_params = sum(p.numel() for p in model.parameters())
+    log(f"built {args.model}: {n_params / 1e9:.3f} B params in {time.time() - t0:.1f}s on {device}")
+
+    if world > 1:
+        bucket = args.bucket_mb if args.bucket_mb is not None else DEFAULT_BUCKET_MB
+        ddp_model = wrap_ddp(model, args.ddp, bucket_size_mb=bucket)
+    else:
+        ddp_model = model
+    if args.sharded and world > 1:
+        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, lr=args.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01)
+    else:
+        opt = ops.FusedAdamW(model.parameters(), lr=args.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01)
+
+    gen = torch.Generator(device=device)
+    gen.manual_seed(1000 + rank)
+    batches = [synthetic_batch(args.batch, args.ctx, args.vocab, device, gen) for _ in range(4)]
+    amp = args.dtype == "bf16" and device.type == "cuda"
+
+    def zero_grads():
+        if hasattr(ddp_model, "zero_grad") and world > 1 and args.ddp in ("bucketed", "flat"):
+            ddp_model.zero_grad()
+        else:
+            opt.zero_grad(set_to_none=True)
+
+    def step(i):
+        x, y = batches[i % len(batches)]
+        zero_grads()
+        with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
+            logits = ddp_model(x)
+            loss = ops.cross_entropy(logits, y)
+        loss.backward()
+        if world > 1:
+            ddp_model.finish_gradient_synchronization()
+        if args.clip > 0:
+            ops.clip_grad_norm_(model.parameters(), args.clip)
+        opt.step()
+        return loss
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for i in range(args.warmup):
+        loss = step(i)
+        sync()
+        log(f"warmup {i}: loss {loss.item():.4f}")
+    if device.type == "cuda":
+        torch.cuda.reset_peak_memory_stats(device)
+    barrier()
+    sync()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(i)
+    sync()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    last_loss = loss.item()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    peak_gib = torch.cuda.max_memory_allocated(device) / 2**30 if device.type == "cuda" else 0.0
+
+    ms_per_step = 1e3 * elapsed / max(args.steps, 1)
+    tokens_per_step = args.batch * args.ctx * world
+    value = tokens_per_step * args.steps / elapsed
+    flops_tok = train_flops_per_token(args.model, args.ctx, args.vocab)
+    mfu = value * flops_tok / (world * 2.5e15)
+    cfg = get_model_config(args.model)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+        "dtype": "bf16" if amp else "fp32",
+        "data": "synthetic (random tokens on device, random-init weights)",
+        "config": {
+            "model": f"{args.model} (GPT-2-XL shape: d_model {cfg['d_model']}, {cfg['num_layers']} layers, {cfg['num_heads']} heads, d_ff {cfg['d_ff']}, vocab {args.vocab}, {param_count(args.model, args.vocab) / 1e9:.2f}B params)",
+            "global_batch": args.batch * world,
+            "per_gpu_batch": args.batch,
+            "seq_len": args.ctx,
+            "parallelism": f"dp{world}" + ("+zero1" if args.sharded and world > 1 else ""),
+            "ddp": args.ddp if world > 1 else "none",
+            "bucket_mb": (args.bucket_mb if args.bucket_mb is not None else DEFAULT_BUCKET_MB) if world > 1 else None,
+            "optimizer": "fused HIP AdamW (fp32 master weights)",
+            "attention": "HIP FlashAttention-2 (causal)",
+        },
+        "mfu_dense_bf16": round(mfu, 4),
+        "model_tflops_per_gpu": round(value * flops_tok / world / 1e12, 1),
+        "peak_mem_gib": round(peak_gib, 2),
+        "final_loss": round(last_loss, 4),
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

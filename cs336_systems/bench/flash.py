@@ -1,0 +1,132 @@
+"""FlashAttention-2 benchmarks (reference ``flashattentioncode.py`` + handout §1.3.2 leaderboard).
+
+Compares the HIP FA2 kernels against the materializing PyTorch attention (and, for context, the
+ROCm PyTorch SDPA) on latency of forward, backward and forward+backward, timed with the HIP-event
+``do_bench`` (cold L2/Infinity Cache between reps). TFLOPS use the standard convention
+fwd = 4·B·H·N²·d (×½ causal), bwd = 2.5 × fwd. Unlike the reference driver, the "HIP" rows really
+are the custom kernels and the requested dtype is honoured (reference bug 7).
+
+    python -m cs336_systems.bench.flash --seq 4096 --d 64 128 --dtype bf16            # BASELINE config 2
+    python -m cs336_systems.bench.flash --sweep                                           # handout sweep
+    python -m cs336_systems.bench.flash --leaderboard                                     # (16,16384,64) causal
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+
+import torch
+
+from ..ops.flash_attention import FlashAttentionHIP, naive_attention
+from ..utils.timing import do_bench
+
+DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
+
+
+def attn_flops(B, H, N, d, causal, mode):
+    f = 4.0 * B * H * N * N * d * (0.5 if causal else 1.0)
+    return {"fwd": f, "bwd": 2.5 * f, "fwd_bwd": 3.5 * f}[mode]
+
+
+def _impls():
+    def hip(q, k, v, causal):
+        return FlashAttentionHIP.apply(q, k, v, causal)
+
+    def naive(q, k, v, causal):
+        return naive_attention(q, k, v, causal)
+
+    def sdpa(q, k, v, causal):
+        return torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=causal)
+
+    return {"hip_fa2": hip, "torch_naive": naive, "torch_sdpa": sdpa}
+
+
+def bench_one(impl: str, B: int, H: int, N: int, d: int, dtype: str, causal: bool, warmup=10, rep=50) -> dict:
+    fn = _impls()[impl]
+    dev = "cuda"
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(B, H, N, d, device=dev, dtype=DT[dtype], requires_grad=True) for _ in range(3))
+    do = torch.randn(B, H, N, d, device=dev, dtype=DT[dtype])
+    row = dict(impl=impl, B=B, H=H, N=N, d=d, dtype=dtype, causal=causal)
+    try:
+        with torch.no_grad():
+            row["fwd_ms"] = do_bench(lambda: fn(q, k, v, causal), warmup=warmup, rep=rep)[0]
+        o = fn(q, k, v, causal)
+        row["bwd_ms"] = do_bench(lambda: torch.autograd.grad(o, (q, k, v), do, retain_graph=True), warmup=warmup, rep=rep)[0]
+
+        def fb():
+            out = fn(q, k, v, causal)
+            torch.autograd.grad(out, (q, k, v), do)
+
+        row["fwd_bwd_ms"] = do_bench(fb, warmup=warmup, rep=rep)[0]
+        for m in ("fwd", "bwd", "fwd_bwd"):
+            row[f"{m}_tflops"] = attn_flops(B, H, N, d, causal, m) / (row[f"{m}_ms"] * 1e-3) / 1e12
+    except torch.OutOfMemoryError:
+        row["error"] = "OOM"
+    del q, k, v, do
+    torch.cuda.empty_cache()
+    return row
+
+
+def leaderboard(compile_fn: bool = True) -> dict:
+    """Handout p.21-22: q,k,v (16, 16384, 64) bf16 causal, fwd+bwd, do_bench(rep=10000, warmup=1000)."""
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(16, 16384, 64, device="cuda", dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    fa = torch.compile(FlashAttentionHIP.apply) if compile_fn else FlashAttentionHIP.apply
+
+    def fb():
+        o = fa(q, k, v, True)
+        loss = o.sum()
+        loss.backward()
+
+    ms = do_bench(fb, warmup=1000, rep=10000, flush_cache=False)[0]
+    return dict(config="leaderboard (16,16384,64) bf16 causal fwd+bwd", ms=ms, tflops=attn_flops(16, 1, 16384, 64, True, "fwd_bwd") / (ms * 1e-3) / 1e12, compiled=compile_fn)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--seq", nargs="+", type=int, default=[4096])
+    ap.add_argument("--d", nargs="+", type=int, default=[64, 128])
+    ap.add_argument("--batch", type=int, default=None, help="default: 16 heads x B with B*N = 16384 tokens")
+    ap.add_argument("--heads", type=int, default=16)
+    ap.add_argument("--dtype", nargs="+", default=["bf16"])
+    ap.add_argument("--causal", nargs="+", type=int, default=[1, 0])
+    ap.add_argument("--impls", nargs="+", default=["hip_fa2", "torch_sdpa", "torch_naive"])
+    ap.add_argument("--sweep", action="store_true", help="seq 128..65536 x d 16..128 x {bf16, fp32}, B=1 (reference sweep)")
+    ap.add_argument("--leaderboard", action="store_true")
+    ap.add_argument("--no-compile", action="store_true")
+    ap.add_argument("--rep", type=int, default=50)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args(argv)
+    rows = []
+    if a.leaderboard:
+        r = leaderboard(not a.no_compile)
+        print(json.dumps(r), flush=True)
+        rows.append(r)
+    else:
+        seqs = [2**i for i in range(7, 17)] if a.sweep else a.seq
+        ds = [16, 32, 64, 128] if a.sweep else a.d
+        dts = ["bf16", "fp32"] if a.sweep else a.dtype
+        for dt in dts:
+            for d in ds:
+                for n in seqs:
+                    for c in a.causal:
+                        for impl in a.impls:
+                            B = 1 if a.sweep else (a.batch or max(1, 16384 // n))
+                            H = 1 if a.sweep else a.heads
+                            if impl == "torch_naive" and B * H * n * n * 4 > 64 * 2**30:
+                                rows.append(dict(impl=impl, N=n, d=d, dtype=dt, causal=bool(c), error="skipped (N^2 too large)"))
+                                continue
+                            r = bench_one(impl, B, H, n, d, dt, bool(c), rep=a.rep)
+                            rows.append(r)
+                            print(json.dumps(r), flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(rows, f, indent=1)
+    return rows
+
+
+if __name__ == "__main__":
+    main()

@@ -48,7 +48,8 @@ class RMSNormHIP(torch.autograd.Function):
 def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-5, out_dtype: torch.dtype | None = None):
     """RMSNorm over the last dim. ``out_dtype`` defaults to the autocast dtype when autocast is on
     (the consumer is a GEMM that would cast anyway), else the input dtype."""
-    if use_hip(x):
+    H = x.shape[-1]
+    if H % 4 == 0 and H <= 8192 and use_hip(x):
         if out_dtype is None:
             out_dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
         return RMSNormHIP.apply(x, weight, eps, out_dtype)

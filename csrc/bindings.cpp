@@ -1,0 +1,351 @@
+// torch.ops.cs336.* registration for the MI355X HIP kernels.
+//
+// Pure TORCH_LIBRARY (no Python headers): the shared library is loaded with
+// torch.ops.load_library, and every op gets a fake impl in cs336_systems/ops/_fake.py so
+// torch.compile can trace through the autograd Functions. Kernels run on the current HIP stream
+// of the tensors' device; nothing here synchronizes the host.
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/library.h>
+
+#include <vector>
+
+#include "cs336/kernels.h"
+
+namespace {
+
+using cs336::DType;
+
+DType to_dtype(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return DType::F32;
+    case at::kBFloat16: return DType::BF16;
+    case at::kHalf: return DType::F16;
+    default: TORCH_CHECK(false, "cs336: unsupported dtype ", t.scalar_type());
+  }
+  return DType::F32;
+}
+
+hipStream_t stream() { return at::hip::getCurrentHIPStream(); }
+
+void check_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "cs336: ", name, " must be a GPU tensor");
+}
+
+// ------------------------------------------------------------------------------------------
+// FlashAttention
+// ------------------------------------------------------------------------------------------
+void check_bhnd(const at::Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.dim() == 4, "cs336: ", name, " must be (B, H, N, D)");
+  TORCH_CHECK(t.stride(3) == 1, "cs336: ", name, " must have a contiguous last dim");
+  const int D = (int)t.size(3);
+  TORCH_CHECK(D == 32 || D == 64 || D == 128, "cs336: head dim must be 32, 64 or 128 (got ", D, ")");
+  const int64_t es = t.element_size();
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) == 0, "cs336: ", name, " must be 16-byte aligned");
+  TORCH_CHECK((t.stride(2) * es) % 16 == 0 && (t.stride(1) * es) % 16 == 0 && (t.stride(0) * es) % 16 == 0,
+              "cs336: ", name, " strides must be multiples of 16 bytes");
+}
+
+// (B,H,N,D) view of freshly allocated (B,N,H,D) memory
+at::Tensor empty_bnhd_like(const at::Tensor& q) {
+  return at::empty({q.size(0), q.size(2), q.size(1), q.size(3)}, q.options()).permute({0, 2, 1, 3});
+}
+
+void fill_attn(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+               const at::Tensor& o, const at::Tensor& lse, bool causal, double scale) {
+  p.q = q.data_ptr();
+  p.k = k.data_ptr();
+  p.v = v.data_ptr();
+  p.o = o.data_ptr();
+  p.lse = lse.data_ptr<float>();
+  p.q_sb = q.stride(0); p.q_sh = q.stride(1); p.q_sn = q.stride(2);
+  p.k_sb = k.stride(0); p.k_sh = k.stride(1); p.k_sn = k.stride(2);
+  p.v_sb = v.stride(0); p.v_sh = v.stride(1); p.v_sn = v.stride(2);
+  p.o_sb = o.stride(0); p.o_sh = o.stride(1); p.o_sn = o.stride(2);
+  p.B = (int)q.size(0);
+  p.H = (int)q.size(1);
+  p.Nq = (int)q.size(2);
+  p.Nk = (int)k.size(2);
+  p.D = (int)q.size(3);
+  p.scale = (float)scale;
+  p.causal = causal;
+}
+
+std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bool causal,
+                                          double scale) {
+  check_bhnd(q, "q");
+  check_bhnd(k, "k");
+  check_bhnd(v, "v");
+  TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(), "cs336: q/k/v dtype mismatch");
+  TORCH_CHECK(k.sizes() == v.sizes(), "cs336: k/v shape mismatch");
+  TORCH_CHECK(q.size(0) == k.size(0) && q.size(1) == k.size(1) && q.size(3) == k.size(3), "cs336: q/k shape mismatch");
+  c10::DeviceGuard g(q.device());
+  at::Tensor o = empty_bnhd_like(q);
+  at::Tensor lse = at::empty({q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
+  cs336::AttnParams p;
+  fill_attn(p, q, k, v, o, lse, causal, scale);
+  cs336::flash_attn_fwd(p, to_dtype(q), stream());
+  return {o, lse};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
+                                                      const at::Tensor& v, const at::Tensor& out,
+                                                      const at::Tensor& lse, bool causal, double scale) {
+  check_bhnd(q, "q");
+  check_bhnd(k, "k");
+  check_bhnd(v, "v");
+  check_bhnd(out, "out");
+  check_bhnd(dout, "dout");
+  TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == at::kFloat, "cs336: lse must be contiguous fp32");
+  TORCH_CHECK(dout.scalar_type() == q.scalar_type() && out.scalar_type() == q.scalar_type(), "cs336: dtype mismatch");
+  c10::DeviceGuard g(q.device());
+  at::Tensor dq = empty_bnhd_like(q);
+  at::Tensor dk = empty_bnhd_like(k);
+  at::Tensor dv = empty_bnhd_like(v);
+  at::Tensor delta = at::empty({q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
+  cs336::AttnBwdParams bp;
+  fill_attn(bp.f, q, k, v, out, lse, causal, scale);
+  bp.dout = dout.data_ptr();
+  bp.do_sb = dout.stride(0); bp.do_sh = dout.stride(1); bp.do_sn = dout.stride(2);
+  bp.dq = dq.data_ptr();
+  bp.dk = dk.data_ptr();
+  bp.dv = dv.data_ptr();
+  bp.dq_sb = dq.stride(0); bp.dq_sh = dq.stride(1); bp.dq_sn = dq.stride(2);
+  bp.dk_sb = dk.stride(0); bp.dk_sh = dk.stride(1); bp.dk_sn = dk.stride(2);
+  bp.dv_sb = dv.stride(0); bp.dv_sh = dv.stride(1); bp.dv_sn = dv.stride(2);
+  bp.delta = delta.data_ptr<float>();
+  cs336::flash_attn_bwd(bp, to_dtype(q), stream());
+  return {dq, dk, dv};
+}
+
+// ------------------------------------------------------------------------------------------
+// RMSNorm
+// ------------------------------------------------------------------------------------------
+std::tuple<at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, double eps,
+                                               std::optional<at::ScalarType> out_dtype) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "cs336: rmsnorm x must be contiguous (M, H)");
+  TORCH_CHECK(w.is_contiguous() && w.numel() == x.size(1), "cs336: rmsnorm weight shape");
+  TORCH_CHECK(x.size(1) % 4 == 0 && x.size(1) <= 8192, "cs336: rmsnorm hidden size must be a multiple of 4, <= 8192");
+  c10::DeviceGuard g(x.device());
+  at::Tensor y = at::empty_like(x, x.options().dtype(out_dtype.value_or(x.scalar_type())));
+  at::Tensor rstd = at::empty({x.size(0)}, x.options().dtype(at::kFloat));
+  if (x.size(0) == 0) return {y, rstd};
+  cs336::rmsnorm_fwd(x.data_ptr(), to_dtype(x), w.data_ptr(), to_dtype(w), y.data_ptr(), to_dtype(y),
+                     rstd.data_ptr<float>(), x.size(0), x.size(1), (float)eps, stream());
+  return {y, rstd};
+}
+
+std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                               const at::Tensor& rstd) {
+  check_cuda(dy, "dy");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "cs336: rmsnorm_bwd shapes");
+  c10::DeviceGuard g(x.device());
+  at::Tensor dx = at::empty_like(x);
+  if (x.size(0) == 0) return {dx, at::zeros({x.size(1)}, x.options().dtype(at::kFloat))};
+  at::Tensor dw = at::empty({x.size(1)}, x.options().dtype(at::kFloat));
+  const int rows = cs336::rmsnorm_bwd_workspace_rows(x.size(0), x.size(1));
+  at::Tensor ws = at::empty({(int64_t)rows, x.size(1)}, x.options().dtype(at::kFloat));
+  cs336::rmsnorm_bwd(dy.data_ptr(), to_dtype(dy), x.data_ptr(), to_dtype(x), w.data_ptr(), to_dtype(w),
+                     rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(), ws.data_ptr<float>(), x.size(0),
+                     x.size(1), stream());
+  return {dx, dw};
+}
+
+// ------------------------------------------------------------------------------------------
+// RoPE
+// ------------------------------------------------------------------------------------------
+at::Tensor rope(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, const std::optional<at::Tensor>& pos,
+                bool inverse) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "cs336: rope x must be (B,H,N,D) with contiguous D");
+  TORCH_CHECK(x.size(3) % 4 == 0, "cs336: rope head dim must be a multiple of 4");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.is_contiguous() && sin.is_contiguous(), "cs336: rope cache");
+  TORCH_CHECK(cos.size(1) * 2 == x.size(3), "cs336: rope cache width");
+  c10::DeviceGuard g(x.device());
+  at::Tensor out = empty_bnhd_like(x);
+  const int64_t* pp = nullptr;
+  if (pos.has_value() && pos->defined()) {
+    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->is_contiguous() && pos->numel() == x.size(0) * x.size(2),
+                "cs336: rope positions must be contiguous int64 (B, N)");
+    pp = pos->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(x.size(2) <= cos.size(0), "cs336: sequence longer than the RoPE cache");
+  }
+  if (x.numel() == 0) return out;
+  cs336::rope(x.data_ptr(), to_dtype(x), x.stride(0), x.stride(1), x.stride(2), out.data_ptr(), cos.data_ptr<float>(),
+              sin.data_ptr<float>(), pp, (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), inverse,
+              stream());
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------
+// SwiGLU gate
+// ------------------------------------------------------------------------------------------
+at::Tensor silu_mul_fwd(const at::Tensor& a, const at::Tensor& b) {
+  check_cuda(a, "a");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && a.sizes() == b.sizes() && a.dtype() == b.dtype(),
+              "cs336: silu_mul operands");
+  c10::DeviceGuard g(a.device());
+  at::Tensor h = at::empty_like(a);
+  cs336::silu_mul_fwd(a.data_ptr(), b.data_ptr(), h.data_ptr(), to_dtype(a), a.numel(), stream());
+  return h;
+}
+
+std::tuple<at::Tensor, at::Tensor> silu_mul_bwd(const at::Tensor& dh, const at::Tensor& a, const at::Tensor& b) {
+  check_cuda(a, "a");
+  TORCH_CHECK(dh.is_contiguous() && dh.sizes() == a.sizes() && dh.dtype() == a.dtype(), "cs336: silu_mul_bwd dh");
+  c10::DeviceGuard g(a.device());
+  at::Tensor da = at::empty_like(a), db = at::empty_like(b);
+  cs336::silu_mul_bwd(dh.data_ptr(), a.data_ptr(), b.data_ptr(), da.data_ptr(), db.data_ptr(), to_dtype(a), a.numel(),
+                      stream());
+  return {da, db};
+}
+
+// ------------------------------------------------------------------------------------------
+// cross entropy
+// ------------------------------------------------------------------------------------------
+std::tuple<at::Tensor, at::Tensor> xent_fwd(const at::Tensor& z, const at::Tensor& t) {
+  check_cuda(z, "logits");
+  TORCH_CHECK(z.dim() == 2 && z.is_contiguous(), "cs336: logits must be contiguous (M, V)");
+  TORCH_CHECK(t.scalar_type() == at::kLong && t.is_contiguous() && t.numel() == z.size(0), "cs336: targets");
+  c10::DeviceGuard g(z.device());
+  at::Tensor loss = at::empty({z.size(0)}, z.options().dtype(at::kFloat));
+  at::Tensor lse = at::empty({z.size(0)}, z.options().dtype(at::kFloat));
+  cs336::xent_fwd(z.data_ptr(), to_dtype(z), t.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(),
+                  z.size(0), z.size(1), stream());
+  return {loss, lse};
+}
+
+at::Tensor xent_bwd(const at::Tensor& gs, const at::Tensor& z, const at::Tensor& t, const at::Tensor& lse,
+                    double mult) {
+  check_cuda(z, "logits");
+  TORCH_CHECK(gs.scalar_type() == at::kFloat && gs.numel() == 1, "cs336: xent_bwd grad must be a fp32 scalar");
+  c10::DeviceGuard g(z.device());
+  at::Tensor dz = at::empty_like(z);
+  cs336::xent_bwd(gs.data_ptr<float>(), z.data_ptr(), to_dtype(z), t.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                  dz.data_ptr(), (float)mult, z.size(0), z.size(1), stream());
+  return dz;
+}
+
+// ------------------------------------------------------------------------------------------
+// multi-tensor
+// ------------------------------------------------------------------------------------------
+struct HostTable {
+  at::Tensor dev;  // keeps the device copy alive until the ops that use it are enqueued
+  cs336::TensorTable tt;
+};
+
+HostTable build_table(const std::vector<std::vector<at::Tensor>>& lists) {
+  const int n = (int)lists[0].size();
+  const int nptr = (int)lists.size();
+  for (const auto& l : lists) TORCH_CHECK((int)l.size() == n, "cs336: tensor lists must have equal length");
+  const int64_t len = (int64_t)n * nptr + (n + 1) + n;
+  at::Tensor host = at::empty({len}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+  int64_t* h = host.data_ptr<int64_t>();
+  int64_t chunks = 0;
+  for (int i = 0; i < n; ++i) {
+    const at::Tensor& t0 = lists[0][i];
+    for (int k = 0; k < nptr; ++k) {
+      const at::Tensor& t = lists[k][i];
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "cs336: multi-tensor inputs must be contiguous GPU tensors");
+      TORCH_CHECK(t.numel() == t0.numel(), "cs336: multi-tensor numel mismatch");
+      h[(int64_t)i * nptr + k] = reinterpret_cast<int64_t>(t.data_ptr());
+    }
+    h[(int64_t)n * nptr + i] = chunks;
+    chunks += (t0.numel() + cs336::kMTChunk - 1) / cs336::kMTChunk;
+    h[(int64_t)n * nptr + (n + 1) + i] = t0.numel();
+  }
+  h[(int64_t)n * nptr + n] = chunks;
+  HostTable ht;
+  ht.dev = host.to(lists[0][0].device(), /*non_blocking=*/true);
+  const int64_t* d = ht.dev.data_ptr<int64_t>();
+  ht.tt.ptrs = d;
+  ht.tt.chunk_base = d + (int64_t)n * nptr;
+  ht.tt.numel = d + (int64_t)n * nptr + (n + 1);
+  ht.tt.n = n;
+  ht.tt.total_chunks = chunks;
+  return ht;
+}
+
+void check_same_dtype(const std::vector<at::Tensor>& ts, at::ScalarType st, const char* name) {
+  for (const auto& t : ts) TORCH_CHECK(t.scalar_type() == st, "cs336: ", name, " dtype mismatch");
+}
+
+void adamw_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> exp_avg,
+                std::vector<at::Tensor> exp_avg_sq, double lr, double beta1, double beta2, double eps,
+                double weight_decay, int64_t step) {
+  if (params.empty()) return;
+  check_same_dtype(params, at::kFloat, "params (fp32 master weights)");
+  check_same_dtype(exp_avg, at::kFloat, "exp_avg");
+  check_same_dtype(exp_avg_sq, at::kFloat, "exp_avg_sq");
+  const at::ScalarType gt = grads[0].scalar_type();
+  check_same_dtype(grads, gt, "grads");
+  c10::DeviceGuard g(params[0].device());
+  HostTable ht = build_table({params, grads, exp_avg, exp_avg_sq});
+  // alpha * (sqrt(1 - b2^t) / (1 - b1^t)) in double, as the reference evaluates it in Python
+  const double alpha_t = lr * (std::sqrt(1.0 - std::pow(beta2, (double)step)) / (1.0 - std::pow(beta1, (double)step)));
+  cs336::adamw_step(ht.tt, to_dtype(grads[0]), (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2),
+                    (float)eps, (float)(lr * weight_decay), (float)alpha_t, stream());
+}
+
+at::Tensor multi_tensor_l2norm(std::vector<at::Tensor> tensors) {
+  TORCH_CHECK(!tensors.empty(), "cs336: empty tensor list");
+  const at::ScalarType st = tensors[0].scalar_type();
+  check_same_dtype(tensors, st, "tensors");
+  c10::DeviceGuard g(tensors[0].device());
+  HostTable ht = build_table({tensors});
+  at::Tensor partials = at::empty({std::max<int64_t>(ht.tt.total_chunks, 1)}, tensors[0].options().dtype(at::kFloat));
+  at::Tensor out = at::zeros({}, tensors[0].options().dtype(at::kFloat));
+  cs336::multi_tensor_sumsq(ht.tt, to_dtype(tensors[0]), partials.data_ptr<float>(), stream());
+  cs336::finalize_l2norm(partials.data_ptr<float>(), ht.tt.total_chunks, out.data_ptr<float>(), stream());
+  return out;
+}
+
+void multi_tensor_scale_(std::vector<at::Tensor> tensors, const at::Tensor& scale) {
+  if (tensors.empty()) return;
+  const at::ScalarType st = tensors[0].scalar_type();
+  check_same_dtype(tensors, st, "tensors");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == 1 && scale.is_cuda(), "cs336: scale");
+  c10::DeviceGuard g(tensors[0].device());
+  HostTable ht = build_table({tensors});
+  cs336::multi_tensor_scale(ht.tt, to_dtype(tensors[0]), scale.data_ptr<float>(), stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(cs336, m) {
+  m.def("fa_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
+  m.def(
+      "fa_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale) -> "
+      "(Tensor, Tensor, Tensor)");
+  m.def("rmsnorm_fwd(Tensor x, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
+  m.def("rope(Tensor x, Tensor cos, Tensor sin, Tensor? pos, bool inverse) -> Tensor");
+  m.def("silu_mul_fwd(Tensor a, Tensor b) -> Tensor");
+  m.def("silu_mul_bwd(Tensor dh, Tensor a, Tensor b) -> (Tensor, Tensor)");
+  m.def("xent_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor)");
+  m.def("xent_bwd(Tensor g, Tensor logits, Tensor targets, Tensor lse, float mult) -> Tensor");
+  m.def(
+      "adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
+      "float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
+  m.def("multi_tensor_l2norm(Tensor[] tensors) -> Tensor");
+  m.def("multi_tensor_scale_(Tensor(a!)[] tensors, Tensor scale) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
+  m.impl("fa_fwd", &fa_fwd);
+  m.impl("fa_bwd", &fa_bwd);
+  m.impl("rmsnorm_fwd", &rmsnorm_fwd);
+  m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+  m.impl("rope", &rope);
+  m.impl("silu_mul_fwd", &silu_mul_fwd);
+  m.impl("silu_mul_bwd", &silu_mul_bwd);
+  m.impl("xent_fwd", &xent_fwd);
+  m.impl("xent_bwd", &xent_bwd);
+  m.impl("adamw_step", &adamw_step);
+  m.impl("multi_tensor_l2norm", &multi_tensor_l2norm);
+  m.impl("multi_tensor_scale_", &multi_tensor_scale_);
+}

@@ -1,0 +1,490 @@
+// FlashAttention-2 backward for MI355X (gfx950 / CDNA4).
+//
+// Parity: reference cs336_systems/flash_attention.py:270-289 (torch.compile of a recompute
+// backward that materializes the full N x N S/P/dP/dS — O(N^2) memory) and the handout's
+// Algorithm 2. Here the backward is O(N) memory, atomics-free and deterministic, as two kernels:
+//
+//  1. fa_bwd_dq   (query-block stationary, like the forward): recomputes S^T = K Q^T and
+//     dP^T = V dO^T per 64-key tile with the query on the MFMA lane, so P = exp2(S*c - L2[q]) and
+//     dS = P (dP - delta[q]) use lane-local row constants; dQ^T += K^T dS^T reuses dS^T straight
+//     from the accumulator as the B operand and gathers K^T with transposed LDS reads of the same
+//     swizzled K image the S^T product reads row-wise. It also computes delta = rowsum(dO * O)
+//     for its rows (written for kernel 2), so no separate preprocessing launch exists.
+//  2. fa_bwd_dkdv (key-block stationary): per 64-query tile S = Q K^T and dP = dO V^T with the
+//     KEY on the lane (cdna_hip_programming.md App. B "Attention backward": their accumulators
+//     are then the B operands of dV^T += dO^T P and dK^T += Q^T dS), Q and dO staged once in
+//     dual-use LDS images (row reads for S/dP, ds_read_b64_tr_b16 for the dO^T/Q^T operands);
+//     the per-query L and delta are staged with the tile and read as float4 per 4 rows.
+// Causal: kernel 1 stops at the diagonal, kernel 2 starts at it; only diagonal tiles are masked.
+#include "fa_common.h"
+
+namespace cs336 {
+namespace fa {
+
+// ============================================================================================
+// dQ (+ delta) kernel
+// ============================================================================================
+template <typename T, int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) {
+  typedef typename Elem<T>::storage S;
+  const AttnParams& p = bp.f;
+  constexpr bool F32 = std::is_same<T, float>::value;
+  constexpr int ES = sizeof(S);
+  constexpr int RB = D * ES, CPR = RB / 16, EPC = 16 / ES;
+  constexpr int BM = 128, BN = 64;
+  constexpr int TILE = BN * RB;
+  constexpr int LPT = BN * CPR / 256;
+  constexpr int NDT = D / 32;
+  constexpr bool PREFETCH = !(F32 && D == 128);
+
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int nqb = (p.Nq + BM - 1) / BM;
+  const int total = nqb * p.B * p.H;
+  const int rid = xcd_remap(blockIdx.x, total);
+  const int bh = rid / nqb;
+  int qb = rid % nqb;
+  if (CAUSAL) qb = nqb - 1 - qb;
+  const int b = bh / p.H, h = bh % p.H;
+  const int q0 = qb * BM;
+  const int qw0 = q0 + wave * 32;
+  const int qrow = qw0 + l32;
+  const bool valid_q = qrow < p.Nq;
+
+  const S* Qp = (const S*)p.q + b * p.q_sb + h * p.q_sh;
+  const S* Kp = (const S*)p.k + b * p.k_sb + h * p.k_sh;
+  const S* Vp = (const S*)p.v + b * p.v_sb + h * p.v_sh;
+  const S* Op = (const S*)p.o + b * p.o_sb + h * p.o_sh;
+  const S* dOp = (const S*)bp.dout + b * bp.do_sb + h * bp.do_sh;
+  S* dQp = (S*)bp.dq + b * bp.dq_sb + h * bp.dq_sh;
+  const int64_t row_lin = ((int64_t)b * p.H + h) * p.Nq + qrow;
+
+  constexpr int NQF = F32 ? D / 8 : D / 16;
+  uint4 qf[NQF], dof[NQF];
+  float delta = 0.f;
+#pragma unroll
+  for (int i = 0; i < NQF; ++i) {
+    const int e = F32 ? (hh * (D / 2) + 4 * i) : (16 * i + 8 * hh);
+    if (valid_q) {
+      qf[i] = *reinterpret_cast<const uint4*>(Qp + (int64_t)qrow * p.q_sn + e);
+      dof[i] = *reinterpret_cast<const uint4*>(dOp + (int64_t)qrow * bp.do_sn + e);
+      // delta partial over this lane's half of d
+#pragma unroll
+      for (int k = 0; k < EPC; k += 4) {
+        const float4 a = load4<T>(dOp + (int64_t)qrow * bp.do_sn + e + k);
+        const float4 c = load4<T>(Op + (int64_t)qrow * p.o_sn + e + k);
+        delta += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
+      }
+    } else {
+      qf[i] = dof[i] = make_uint4(0, 0, 0, 0);
+    }
+  }
+  delta += __shfl_xor(delta, 32, 64);
+  const float lse2 = valid_q ? p.lse[row_lin] * kLog2e : INFINITY;
+  if (valid_q && hh == 0) bp.delta[row_lin] = delta;
+
+  const int kv_end = CAUSAL ? min(p.Nk, q0 + BM) : p.Nk;
+  const int ntiles = (kv_end + BN - 1) / BN;
+
+  uint4 kst[LPT], vst[LPT];
+  auto gload = [&](int j) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / CPR, ch = c % CPR;
+      const int key = j * BN + r;
+      if (key < p.Nk) {
+        kst[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)key * p.k_sn + ch * EPC);
+        vst[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)key * p.v_sn + ch * EPC);
+      } else {
+        kst[i] = vst[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* Ks = smem + buf * 2 * TILE;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i;
+      const int off = lds_off<RB>(c / CPR, c % CPR);
+      *reinterpret_cast<uint4*>(Ks + off) = kst[i];
+      *reinterpret_cast<uint4*>(Ks + TILE + off) = vst[i];
+    }
+  };
+
+  f32x16 dq[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) dq[i] = zero16();
+  const float c2 = p.scale * kLog2e;
+
+  if (ntiles > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+
+  for (int j = 0; j < ntiles; ++j) {
+    const int buf = PREFETCH ? (j & 1) : 0;
+    if (PREFETCH && j + 1 < ntiles) gload(j + 1);
+    const int kt0 = j * BN;
+    const bool active = !CAUSAL || kt0 <= qw0 + 31;
+    if (active) {
+      const char* Ks = smem + buf * 2 * TILE;
+      const char* Vs = Ks + TILE;
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        s[t] = zero16();
+        dp[t] = zero16();
+        if constexpr (F32) {
+#pragma unroll
+          for (int i = 0; i < D / 8; ++i) {
+            const float4 kv = lds_f4<RB>(Ks, 32 * t + l32, hh * (D / 2) + 4 * i);
+            const float4 vv = lds_f4<RB>(Vs, 32 * t + l32, hh * (D / 2) + 4 * i);
+            const float4 qv = __builtin_bit_cast(float4, qf[i]);
+            const float4 gv = __builtin_bit_cast(float4, dof[i]);
+            s[t] = mma_f32(kv.x, qv.x, s[t]);
+            s[t] = mma_f32(kv.y, qv.y, s[t]);
+            s[t] = mma_f32(kv.z, qv.z, s[t]);
+            s[t] = mma_f32(kv.w, qv.w, s[t]);
+            dp[t] = mma_f32(vv.x, gv.x, dp[t]);
+            dp[t] = mma_f32(vv.y, gv.y, dp[t]);
+            dp[t] = mma_f32(vv.z, gv.z, dp[t]);
+            dp[t] = mma_f32(vv.w, gv.w, dp[t]);
+          }
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < D / 16; ++ks) {
+            s[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Ks, 32 * t, ks, lane), as_frag<T>(qf[ks]), s[t]);
+            dp[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Vs, 32 * t, ks, lane), as_frag<T>(dof[ks]), dp[t]);
+          }
+        }
+      }
+      const bool need_mask = (kt0 + BN > p.Nk) || (CAUSAL && kt0 + BN - 1 > qw0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float pv = fexp2(fmaf(s[t][r], c2, -lse2));
+          if (need_mask) {
+            const int key = kt0 + 32 * t + acc_row(r, hh);
+            if (key >= p.Nk || (CAUSAL && key > qrow)) pv = 0.f;
+          }
+          s[t][r] = pv * (dp[t][r] - delta);  // dS^T
+        }
+      if constexpr (F32) {
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              dq[dt] = mma_f32(lds_f1<RB>(Ks, 32 * t + acc_row(r, hh), dt * 32 + l32), s[t][r], dq[dt]);
+      } else {
+        typename Mma16<T>::frag pf[2][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          pf[t][0] = pack_acc<T>(s[t], 0);
+          pf[t][1] = pack_acc<T>(s[t], 1);
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+              dq[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Ks, 32 * t, s2, dt, lane), pf[t][s2], dq[dt]);
+      }
+    }
+    if (j + 1 < ntiles) {
+      if (PREFETCH) {
+        swrite(buf ^ 1);
+      } else {
+        __syncthreads();
+        gload(j + 1);
+        swrite(0);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (valid_q) {
+    S* row = dQp + (int64_t)qrow * bp.dq_sn;
+    const float sc = p.scale;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        store4<T>(row + d, make_float4(dq[dt][4 * g] * sc, dq[dt][4 * g + 1] * sc, dq[dt][4 * g + 2] * sc,
+                                       dq[dt][4 * g + 3] * sc));
+      }
+  }
+}
+
+// ============================================================================================
+// dK / dV kernel
+// ============================================================================================
+template <typename T, int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp) {
+  typedef typename Elem<T>::storage S;
+  const AttnParams& p = bp.f;
+  constexpr bool F32 = std::is_same<T, float>::value;
+  constexpr int ES = sizeof(S);
+  constexpr int RB = D * ES, CPR = RB / 16, EPC = 16 / ES;
+  constexpr int BK = 128, BQ = 64;
+  constexpr int TILE = BQ * RB;
+  constexpr int BUF = 2 * TILE + 2 * BQ * 4;  // Q, dO images + L2, delta rows
+  constexpr int LPT = BQ * CPR / 256;
+  constexpr int NDT = D / 32;
+  constexpr bool PREFETCH = D <= 64;
+
+  __shared__ __attribute__((aligned(16))) char smem[(PREFETCH ? 2 : 1) * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int nkb = (p.Nk + BK - 1) / BK;
+  const int total = nkb * p.B * p.H;
+  const int rid = xcd_remap(blockIdx.x, total);
+  const int bh = rid / nkb;
+  const int kb = rid % nkb;  // ascending = heaviest first under the causal mask
+  const int b = bh / p.H, h = bh % p.H;
+  const int k0 = kb * BK;
+  const int kw0 = k0 + wave * 32;
+  const int krow = kw0 + l32;
+  const bool valid_k = krow < p.Nk;
+
+  const S* Qp = (const S*)p.q + b * p.q_sb + h * p.q_sh;
+  const S* Kp = (const S*)p.k + b * p.k_sb + h * p.k_sh;
+  const S* Vp = (const S*)p.v + b * p.v_sb + h * p.v_sh;
+  const S* dOp = (const S*)bp.dout + b * bp.do_sb + h * bp.do_sh;
+  const float* Lp = p.lse + ((int64_t)b * p.H + h) * p.Nq;
+  const float* Dp = bp.delta + ((int64_t)b * p.H + h) * p.Nq;
+  S* dKp = (S*)bp.dk + b * bp.dk_sb + h * bp.dk_sh;
+  S* dVp = (S*)bp.dv + b * bp.dv_sb + h * bp.dv_sh;
+
+  // K, V fragments (B operands), resident
+  constexpr int NKF = F32 ? D / 8 : D / 16;
+  uint4 kf[NKF], vf[NKF];
+#pragma unroll
+  for (int i = 0; i < NKF; ++i) {
+    const int e = F32 ? (hh * (D / 2) + 4 * i) : (16 * i + 8 * hh);
+    if (valid_k) {
+      kf[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)krow * p.k_sn + e);
+      vf[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)krow * p.v_sn + e);
+    } else {
+      kf[i] = vf[i] = make_uint4(0, 0, 0, 0);
+    }
+  }
+
+  const int qt_begin = CAUSAL ? (k0 / BQ) : 0;
+  const int qt_end = (p.Nq + BQ - 1) / BQ;
+
+  uint4 qst[LPT], dst[LPT];
+  float lst = 0.f, dlt = 0.f;
+  auto gload = [&](int it) {
+    const int qbase = it * BQ;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / CPR, ch = c % CPR;
+      const int q = qbase + r;
+      if (q < p.Nq) {
+        qst[i] = *reinterpret_cast<const uint4*>(Qp + (int64_t)q * p.q_sn + ch * EPC);
+        dst[i] = *reinterpret_cast<const uint4*>(dOp + (int64_t)q * bp.do_sn + ch * EPC);
+      } else {
+        qst[i] = dst[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    if (tid < BQ) {
+      const int q = qbase + tid;
+      lst = q < p.Nq ? Lp[q] * kLog2e : INFINITY;
+      dlt = q < p.Nq ? Dp[q] : 0.f;
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* base = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i;
+      const int off = lds_off<RB>(c / CPR, c % CPR);
+      *reinterpret_cast<uint4*>(base + off) = qst[i];
+      *reinterpret_cast<uint4*>(base + TILE + off) = dst[i];
+    }
+    if (tid < BQ) {
+      reinterpret_cast<float*>(base + 2 * TILE)[tid] = lst;
+      reinterpret_cast<float*>(base + 2 * TILE + BQ * 4)[tid] = dlt;
+    }
+  };
+
+  f32x16 dk[NDT], dv[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) {
+    dk[i] = zero16();
+    dv[i] = zero16();
+  }
+  const float c2 = p.scale * kLog2e;
+
+  if (qt_begin < qt_end) {
+    gload(qt_begin);
+    swrite(0);
+  }
+  __syncthreads();
+
+  for (int it = qt_begin; it < qt_end; ++it) {
+    const int buf = PREFETCH ? ((it - qt_begin) & 1) : 0;
+    if (PREFETCH && it + 1 < qt_end) gload(it + 1);
+    const int qt0 = it * BQ;
+    const bool active = !CAUSAL || (qt0 + BQ - 1 >= kw0);
+    if (active) {
+      const char* Qs = smem + buf * BUF;
+      const char* dOs = Qs + TILE;
+      const float* Ls = reinterpret_cast<const float*>(Qs + 2 * TILE);
+      const float* Ds = Ls + BQ;
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        s[t] = zero16();
+        dp[t] = zero16();
+        if constexpr (F32) {
+#pragma unroll
+          for (int i = 0; i < D / 8; ++i) {
+            const float4 qv = lds_f4<RB>(Qs, 32 * t + l32, hh * (D / 2) + 4 * i);
+            const float4 gv = lds_f4<RB>(dOs, 32 * t + l32, hh * (D / 2) + 4 * i);
+            const float4 kv = __builtin_bit_cast(float4, kf[i]);
+            const float4 vv = __builtin_bit_cast(float4, vf[i]);
+            s[t] = mma_f32(qv.x, kv.x, s[t]);
+            s[t] = mma_f32(qv.y, kv.y, s[t]);
+            s[t] = mma_f32(qv.z, kv.z, s[t]);
+            s[t] = mma_f32(qv.w, kv.w, s[t]);
+            dp[t] = mma_f32(gv.x, vv.x, dp[t]);
+            dp[t] = mma_f32(gv.y, vv.y, dp[t]);
+            dp[t] = mma_f32(gv.z, vv.z, dp[t]);
+            dp[t] = mma_f32(gv.w, vv.w, dp[t]);
+          }
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < D / 16; ++ks) {
+            s[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Qs, 32 * t, ks, lane), as_frag<T>(kf[ks]), s[t]);
+            dp[t] = Mma16<T>::mma(lds_row_frag<T, RB>(dOs, 32 * t, ks, lane), as_frag<T>(vf[ks]), dp[t]);
+          }
+        }
+      }
+      // P = exp2(S*c - L2[q]); dS = P (dP - delta[q]); rows (q) are in registers
+      const bool need_mask = CAUSAL && (qt0 < kw0 + 31);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int qr = 32 * t + 8 * g + 4 * hh;
+          const float4 L4 = *reinterpret_cast<const float4*>(Ls + qr);
+          const float4 D4 = *reinterpret_cast<const float4*>(Ds + qr);
+          const float Lv[4] = {L4.x, L4.y, L4.z, L4.w};
+          const float Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = 4 * g + u;
+            float pv = fexp2(fmaf(s[t][r], c2, -Lv[u]));
+            if (need_mask && (krow > qt0 + qr + u)) pv = 0.f;
+            s[t][r] = pv;
+            dp[t][r] = pv * (dp[t][r] - Dv[u]);
+          }
+        }
+      if constexpr (F32) {
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int qr = 32 * t + acc_row(r, hh);
+              dv[dt] = mma_f32(lds_f1<RB>(dOs, qr, dt * 32 + l32), s[t][r], dv[dt]);
+              dk[dt] = mma_f32(lds_f1<RB>(Qs, qr, dt * 32 + l32), dp[t][r], dk[dt]);
+            }
+      } else {
+        typename Mma16<T>::frag pf[2][2], sf[2][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          pf[t][0] = pack_acc<T>(s[t], 0);
+          pf[t][1] = pack_acc<T>(s[t], 1);
+          sf[t][0] = pack_acc<T>(dp[t], 0);
+          sf[t][1] = pack_acc<T>(dp[t], 1);
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+              dv[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(dOs, 32 * t, s2, dt, lane), pf[t][s2], dv[dt]);
+              dk[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Qs, 32 * t, s2, dt, lane), sf[t][s2], dk[dt]);
+            }
+      }
+    }
+    if (it + 1 < qt_end) {
+      if (PREFETCH) {
+        swrite(buf ^ 1);
+      } else {
+        __syncthreads();
+        gload(it + 1);
+        swrite(0);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (valid_k) {
+    S* krow_dk = dKp + (int64_t)krow * bp.dk_sn;
+    S* krow_dv = dVp + (int64_t)krow * bp.dv_sn;
+    const float sc = p.scale;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        store4<T>(krow_dk + d, make_float4(dk[dt][4 * g] * sc, dk[dt][4 * g + 1] * sc, dk[dt][4 * g + 2] * sc,
+                                           dk[dt][4 * g + 3] * sc));
+        store4<T>(krow_dv + d, make_float4(dv[dt][4 * g], dv[dt][4 * g + 1], dv[dt][4 * g + 2], dv[dt][4 * g + 3]));
+      }
+  }
+}
+
+template <typename T, int D>
+void launch_bwd(const AttnBwdParams& bp, hipStream_t s) {
+  const AttnParams& p = bp.f;
+  const int nqb = (p.Nq + 127) / 128;
+  const int nkb = (p.Nk + 127) / 128;
+  const dim3 gq((unsigned)(nqb * p.B * p.H)), gk((unsigned)(nkb * p.B * p.H)), block(256);
+  if (p.causal) {
+    hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, true>), gq, block, 0, s, bp);
+    hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, true>), gk, block, 0, s, bp);
+  } else {
+    hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, false>), gq, block, 0, s, bp);
+    hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, false>), gk, block, 0, s, bp);
+  }
+}
+
+template <typename T>
+void launch_bwd_d(const AttnBwdParams& bp, hipStream_t s) {
+  switch (bp.f.D) {
+    case 32: launch_bwd<T, 32>(bp, s); break;
+    case 64: launch_bwd<T, 64>(bp, s); break;
+    case 128: launch_bwd<T, 128>(bp, s); break;
+    default: fprintf(stderr, "fa_bwd: unsupported head dim %d\n", bp.f.D); abort();
+  }
+}
+
+}  // namespace fa
+
+void flash_attn_bwd(const AttnBwdParams& bp, DType t, hipStream_t s) {
+  if (bp.f.B * bp.f.H == 0 || bp.f.Nq == 0 || bp.f.Nk == 0) return;
+  switch (t) {
+    case DType::BF16: fa::launch_bwd_d<BF16>(bp, s); break;
+    case DType::F16: fa::launch_bwd_d<F16>(bp, s); break;
+    case DType::F32: fa::launch_bwd_d<float>(bp, s); break;
+  }
+}
+
+}  // namespace cs336

@@ -1,0 +1,168 @@
+// Shared building blocks of the CDNA4 FlashAttention-2 kernels (fa_fwd.hip, fa_bwd.hip).
+//
+// MFMA shapes: 16-bit inputs use v_mfma_f32_32x32x16_{bf16,f16}; fp32 inputs use the exact
+// f32-in/f32-acc v_mfma_f32_32x32x2_f32 (no TF32-like shortcut exists on gfx950, and the
+// 1e-2-tolerance fp32 tests deserve exact products).
+//
+// "Key on the register, query on the lane": every score tile is computed *transposed*
+// (S^T = K Q^T, C[key][q]), so a lane owns one query row and its running max / sum / rescale are
+// lane-local (one cross-half exchange per tile for the max). The S^T accumulator is then directly
+// the B operand of the next MFMA (O^T += V^T P^T), see cdna_hip_programming.md §3 "An accumulator
+// tile as the next MFMA's operand": registers 8s..8s+7 packed to bf16 are k-step s, whose k order
+// is key = 16s + 8(j>>2) + 4h + (j&3); the V^T operand is gathered in exactly that key order with
+// ds_read_b64_tr_b16 hardware-transposed LDS reads.
+//
+// LDS images: one XOR swizzle on 16-byte chunks (function of the row length) makes BOTH the
+// row-fragment reads (ds_read_b128, 16 lanes on 16 different rows) and the transposed reads
+// (ds_read_b64_tr_b16, a 32-lane half on 4 rows x 64 B) bank-conflict free, so a K (or Q/dO)
+// tile staged once serves row-wise and column-wise consumers (T2 + T10 of the guide).
+#pragma once
+
+#include "cs336/common.h"
+#include "cs336/kernels.h"
+
+namespace cs336 {
+namespace fa {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kNegBig = -1e30f;
+// Online-softmax rescale threshold in log2 units (guide T13): the running max is only raised
+// (and O, l rescaled) when some row's tile max exceeds it by more than this, so P <= 2^8.
+constexpr float kRescaleThr = 8.f;
+
+// raw v_exp_f32 (2^x); exp2f() adds a denormal-range fixup sequence we do not need here
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// wave index as a provably wave-uniform (SGPR) value, so per-wave tile skips / mask decisions
+// compile to scalar branches instead of predicated vector code
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// ---- swizzle: physical 16-B chunk = chunk ^ swz(row) --------------------------------------
+template <int RB>
+__device__ __forceinline__ int swz(int r) {
+  if constexpr (RB == 64) {
+    return (r >> 2) & 3;
+  } else if constexpr (RB == 128) {
+    const int g = (r >> 1) & 7;
+    return g ^ ((g & 1) << 2);
+  } else {
+    return ((r & 3) << 2) | ((r >> 2) & 3);
+  }
+}
+template <int RB>
+__device__ __forceinline__ int lds_off(int r, int chunk) {
+  return r * RB + ((chunk ^ swz<RB>(r)) << 4);
+}
+
+// ---- 16-bit MFMA traits ------------------------------------------------------------------
+template <typename T> struct Mma16;
+template <> struct Mma16<BF16> {
+  typedef bf16x8 frag;
+  static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ frag pack(float x0, float x1, float x2, float x3, float x4, float x5, float x6,
+                                              float x7) {
+    frag f;
+    f[0] = (__bf16)x0; f[1] = (__bf16)x1; f[2] = (__bf16)x2; f[3] = (__bf16)x3;
+    f[4] = (__bf16)x4; f[5] = (__bf16)x5; f[6] = (__bf16)x6; f[7] = (__bf16)x7;
+    return f;
+  }
+};
+template <> struct Mma16<F16> {
+  typedef f16x8 frag;
+  static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ frag pack(float x0, float x1, float x2, float x3, float x4, float x5, float x6,
+                                              float x7) {
+    frag f;
+    f[0] = (_Float16)x0; f[1] = (_Float16)x1; f[2] = (_Float16)x2; f[3] = (_Float16)x3;
+    f[4] = (_Float16)x4; f[5] = (_Float16)x5; f[6] = (_Float16)x6; f[7] = (_Float16)x7;
+    return f;
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ typename Mma16<T>::frag as_frag(uint4 u) {
+  return __builtin_bit_cast(typename Mma16<T>::frag, u);
+}
+
+// pack accumulator registers 8s..8s+7 of a 32x32 tile into the bf16/f16 operand of k-step s
+template <typename T>
+__device__ __forceinline__ typename Mma16<T>::frag pack_acc(const f32x16& a, int s) {
+  return Mma16<T>::pack(a[8 * s + 0], a[8 * s + 1], a[8 * s + 2], a[8 * s + 3], a[8 * s + 4], a[8 * s + 5],
+                        a[8 * s + 6], a[8 * s + 7]);
+}
+
+__device__ __forceinline__ f32x16 mma_f32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// Row fragment (A operand of a 32x32x16 MFMA over a [row][d] LDS image): lane reads row
+// `row0 + (lane&31)`, 8 elements starting at d = 16*ks + 8*(lane>>5).
+template <typename T, int RB>
+__device__ __forceinline__ typename Mma16<T>::frag lds_row_frag(const char* img, int row0, int ks, int lane) {
+  const int r = row0 + (lane & 31);
+  const int chunk = 2 * ks + (lane >> 5);
+  return as_frag<T>(*reinterpret_cast<const uint4*>(img + lds_off<RB>(r, chunk)));
+}
+
+// Transposed fragment (A operand = image^T): lane (d = dt*32 + (lane&31), half h) gets the 8
+// elements image[row0 + 16s + 8(j>>2) + 4h + (j&3)][d], j = 0..7, via two ds_read_b64_tr_b16.
+template <typename T, int RB>
+__device__ __forceinline__ typename Mma16<T>::frag lds_tr_frag(const char* img, int row0, int s, int dt, int lane) {
+  const int i = lane & 15, gq = (lane >> 4) & 1, h = lane >> 5;
+  const int chunk = dt * 4 + gq * 2 + ((i & 3) >> 1);
+  const int within = (i & 1) * 8;
+  const int ra = row0 + 16 * s + 4 * h + (i >> 2);
+  const int rb = ra + 8;
+  const lds_s16x4* pa = (const lds_s16x4*)(img + lds_off<RB>(ra, chunk) + within);
+  const lds_s16x4* pb = (const lds_s16x4*)(img + lds_off<RB>(rb, chunk) + within);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)pa);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)pb);
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return __builtin_bit_cast(typename Mma16<T>::frag, v);
+}
+
+// f32 images: 4 consecutive floats of row r starting at element e (e % 4 == 0)
+template <int RB>
+__device__ __forceinline__ float4 lds_f4(const char* img, int r, int e) {
+  return *reinterpret_cast<const float4*>(img + lds_off<RB>(r, e >> 2));
+}
+template <int RB>
+__device__ __forceinline__ float lds_f1(const char* img, int r, int e) {
+  return *reinterpret_cast<const float*>(img + lds_off<RB>(r, e >> 2) + ((e & 3) << 2));
+}
+
+// key (or row) index held by accumulator register `reg` of lane-half h in a 32x32 tile
+__device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// Bijective XCD-aware remap of a 1-D block id: blocks that share a (batch, head) — and hence the
+// same K/V (or Q/dO) stream — become contiguous in the remapped order, i.e. share one XCD's L2
+// (guide T1, bijective variant for totals not divisible by 8).
+__device__ __forceinline__ int xcd_remap(int bid, int total) {
+  const int xcd = bid & 7, q = total >> 3, r = total & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+}  // namespace fa
+}  // namespace cs336

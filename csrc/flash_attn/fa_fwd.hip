@@ -1,0 +1,263 @@
+// FlashAttention-2 forward for MI355X (gfx950 / CDNA4).
+//
+// Parity: reference cs336_systems/flash_attention.py:137-266 (Triton kernel, 16x16 tiles) and the
+// handout's Algorithm 1. Design here is CDNA4-first:
+//   * workgroup = 4 waves = 128 query rows (32 per wave, one query row per MFMA lane column);
+//     grid = (query blocks) x (batch*heads), 1-D with an XCD-aware remap so one head's blocks
+//     share an L2, causal blocks dispatched heaviest-first;
+//   * K/V tiles of 64 keys are staged global -> registers -> swizzled LDS, double-buffered with
+//     the next tile's global loads issued before the current tile's MFMAs (T14 split);
+//   * S^T = K Q^T on v_mfma_f32_32x32x16_{bf16,f16} (exact v_mfma_f32_32x32x2_f32 for fp32),
+//     online softmax in registers with exp2 and the scale folded into one FMA, P^T packed from the
+//     accumulator straight into the PV MFMA's B operand, V^T gathered by ds_read_b64_tr_b16;
+//   * causal: tiles above the diagonal are never loaded (kv_end = q0 + 128), waves skip tiles
+//     entirely above their rows, and only tiles straddling the diagonal pay the mask.
+// Output O keeps the input dtype and is written through arbitrary (batch, head, seq) strides;
+// LSE (natural log, fp32, (B,H,Nq)) is the single extra tensor the backward needs.
+#include "fa_common.h"
+
+namespace cs336 {
+namespace fa {
+
+template <typename T, int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
+  typedef typename Elem<T>::storage S;
+  constexpr bool F32 = std::is_same<T, float>::value;
+  constexpr int ES = sizeof(S);
+  constexpr int RB = D * ES;       // bytes per row
+  constexpr int CPR = RB / 16;     // 16-byte chunks per row
+  constexpr int EPC = 16 / ES;     // elements per chunk
+  constexpr int BM = 128, BN = 64;
+  constexpr int TILE = BN * RB;
+  constexpr int LPT = BN * CPR / 256;  // 16-B staging loads per thread per tile
+  constexpr int NDT = D / 32;          // 32-wide d tiles of O^T
+  constexpr bool PREFETCH = !(F32 && D == 128);
+
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int l32 = lane & 31, hh = lane >> 5;
+
+  const int nqb = (p.Nq + BM - 1) / BM;
+  const int total = nqb * p.B * p.H;
+  const int rid = xcd_remap(blockIdx.x, total);
+  const int bh = rid / nqb;
+  int qb = rid % nqb;
+  if (CAUSAL) qb = nqb - 1 - qb;
+  const int b = bh / p.H, h = bh % p.H;
+  const int q0 = qb * BM;
+
+  const S* Qp = (const S*)p.q + b * p.q_sb + h * p.q_sh;
+  const S* Kp = (const S*)p.k + b * p.k_sb + h * p.k_sh;
+  const S* Vp = (const S*)p.v + b * p.v_sb + h * p.v_sh;
+  S* Op = (S*)p.o + b * p.o_sb + h * p.o_sh;
+
+  const int qw0 = q0 + wave * 32;
+  const int qrow = qw0 + l32;
+  const bool valid_q = qrow < p.Nq;
+
+  // ---- Q fragments (B operand), resident for the whole kernel -------------------------------
+  constexpr int NQF = F32 ? D / 8 : D / 16;  // uint4 per lane
+  uint4 qf[NQF];
+#pragma unroll
+  for (int i = 0; i < NQF; ++i) {
+    // 16-bit: chunk 2*ks + hh  |  f32: d = hh*D/2 + 4*i .. +3
+    const int e = F32 ? (hh * (D / 2) + 4 * i) : (16 * i + 8 * hh);
+    qf[i] = valid_q ? *reinterpret_cast<const uint4*>(Qp + (int64_t)qrow * p.q_sn + e) : make_uint4(0, 0, 0, 0);
+  }
+
+  const int kv_end = CAUSAL ? min(p.Nk, q0 + BM) : p.Nk;
+  const int ntiles = (kv_end + BN - 1) / BN;
+
+  uint4 kst[LPT], vst[LPT];
+  auto gload = [&](int j) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / CPR, ch = c % CPR;
+      const int key = j * BN + r;
+      if (key < p.Nk) {
+        kst[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)key * p.k_sn + ch * EPC);
+        vst[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)key * p.v_sn + ch * EPC);
+      } else {
+        kst[i] = make_uint4(0, 0, 0, 0);
+        vst[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* Ks = smem + buf * 2 * TILE;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / CPR, ch = c % CPR;
+      const int off = lds_off<RB>(r, ch);
+      *reinterpret_cast<uint4*>(Ks + off) = kst[i];
+      *reinterpret_cast<uint4*>(Ks + TILE + off) = vst[i];
+    }
+  };
+
+  float m = kNegBig, l = 0.f;
+  f32x16 o[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) o[i] = zero16();
+  const float c2 = p.scale * kLog2e;
+
+  if (ntiles > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+
+  for (int j = 0; j < ntiles; ++j) {
+    const int buf = PREFETCH ? (j & 1) : 0;
+    if (PREFETCH && j + 1 < ntiles) gload(j + 1);
+    const int kt0 = j * BN;
+    const bool active = !CAUSAL || kt0 <= qw0 + 31;
+    if (active) {
+      const char* Ks = smem + buf * 2 * TILE;
+      const char* Vs = Ks + TILE;
+      f32x16 s[2];
+      // ---- S^T = K Q^T ----
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        s[t] = zero16();
+        if constexpr (F32) {
+#pragma unroll
+          for (int i = 0; i < D / 8; ++i) {
+            const float4 kv = lds_f4<RB>(Ks, 32 * t + l32, hh * (D / 2) + 4 * i);
+            const float4 qv = __builtin_bit_cast(float4, qf[i]);
+            s[t] = mma_f32(kv.x, qv.x, s[t]);
+            s[t] = mma_f32(kv.y, qv.y, s[t]);
+            s[t] = mma_f32(kv.z, qv.z, s[t]);
+            s[t] = mma_f32(kv.w, qv.w, s[t]);
+          }
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < D / 16; ++ks)
+            s[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Ks, 32 * t, ks, lane), as_frag<T>(qf[ks]), s[t]);
+        }
+      }
+      // ---- mask (bounds / causal diagonal) ----
+      const bool need_mask = (kt0 + BN > p.Nk) || (CAUSAL && kt0 + BN - 1 > qw0);
+      if (need_mask) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kt0 + 32 * t + acc_row(r, hh);
+            if (key >= p.Nk || (CAUSAL && key > qrow)) s[t][r] = -INFINITY;
+          }
+      }
+      // ---- online softmax (query on the lane), deferred rescale (T13) ----
+      float mx = s[0][0];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[t][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mt = mx * c2;
+      if (__ballot(mt > m + kRescaleThr) != 0) {  // wave-uniform
+        const float m_new = fmaxf(m, mt);
+        const float alpha = fexp2(m - m_new);
+        l *= alpha;
+        m = m_new;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+      }
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fexp2(fmaf(s[t][r], c2, -m));
+          s[t][r] = pv;
+          rs += pv;
+        }
+      l += rs;
+      // ---- O^T += V^T P^T ----
+      if constexpr (F32) {
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              o[dt] = mma_f32(lds_f1<RB>(Vs, 32 * t + acc_row(r, hh), dt * 32 + l32), s[t][r], o[dt]);
+      } else {
+        typename Mma16<T>::frag pf[2][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          pf[t][0] = pack_acc<T>(s[t], 0);
+          pf[t][1] = pack_acc<T>(s[t], 1);
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+              o[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Vs, 32 * t, s2, dt, lane), pf[t][s2], o[dt]);
+      }
+    }
+    if (j + 1 < ntiles) {
+      if (PREFETCH) {
+        swrite(buf ^ 1);
+      } else {
+        __syncthreads();
+        gload(j + 1);
+        swrite(0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  l += __shfl_xor(l, 32, 64);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (valid_q) {
+    S* orow = Op + (int64_t)qrow * p.o_sn;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        store4<T>(orow + d, make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
+                                        o[dt][4 * g + 3] * inv));
+      }
+    if (hh == 0) p.lse[((int64_t)b * p.H + h) * p.Nq + qrow] = l > 0.f ? (m + __log2f(l)) * kLn2 : -INFINITY;
+  }
+}
+
+template <typename T, int D>
+void launch_fwd(const AttnParams& p, hipStream_t s) {
+  const int nqb = (p.Nq + 127) / 128;
+  const dim3 grid((unsigned)(nqb * p.B * p.H)), block(256);
+  if (p.causal) hipLaunchKernelGGL((fa_fwd_kernel<T, D, true>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((fa_fwd_kernel<T, D, false>), grid, block, 0, s, p);
+}
+
+template <typename T>
+void launch_fwd_d(const AttnParams& p, hipStream_t s) {
+  switch (p.D) {
+    case 32: launch_fwd<T, 32>(p, s); break;
+    case 64: launch_fwd<T, 64>(p, s); break;
+    case 128: launch_fwd<T, 128>(p, s); break;
+    default: fprintf(stderr, "fa_fwd: unsupported head dim %d\n", p.D); abort();
+  }
+}
+
+}  // namespace fa
+
+void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s) {
+  if (p.B * p.H == 0 || p.Nq == 0) return;
+  switch (t) {
+    case DType::BF16: fa::launch_fwd_d<BF16>(p, s); break;
+    case DType::F16: fa::launch_fwd_d<F16>(p, s); break;
+    case DType::F32: fa::launch_fwd_d<float>(p, s); break;
+  }
+}
+
+}  // namespace cs336

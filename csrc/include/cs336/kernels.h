@@ -1,0 +1,88 @@
+// Host-side launchers of the cs336 HIP kernels. These take raw device pointers + a HIP stream and
+// have no PyTorch dependency; csrc/bindings.cpp adapts them to torch.ops.cs336.*.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace cs336 {
+
+// ---- RMSNorm (csrc/ops/rmsnorm.hip) ----
+void rmsnorm_fwd(const void* x, DType xt, const void* w, DType wt, void* y, DType yt, float* rstd, int64_t M,
+                 int64_t H, float eps, hipStream_t s);
+// dx (dtype xt); dw (fp32, H) via a (rows x H) fp32 workspace of per-workgroup partials
+void rmsnorm_bwd(const void* dy, DType dyt, const void* x, DType xt, const void* w, DType wt, const float* rstd,
+                 void* dx, float* dw, float* workspace, int64_t M, int64_t H, hipStream_t s);
+int rmsnorm_bwd_workspace_rows(int64_t M, int64_t H);
+
+// ---- RoPE (csrc/ops/rope.hip) ----
+// x: (B,H,N,D) strided (elements), out: contiguous (B,N,H,D); cos/sin: (ctx, D/2) fp32;
+// pos: (B,N) int64 or nullptr (position = n).
+void rope(const void* x, DType t, int64_t sb, int64_t sh, int64_t sn, void* out, const float* cos_, const float* sin_,
+          const int64_t* pos, int B, int H, int N, int D, bool inverse, hipStream_t s);
+
+// ---- SwiGLU gate (csrc/ops/swiglu.hip) ----
+void silu_mul_fwd(const void* a, const void* b, void* h, DType t, int64_t n, hipStream_t s);
+void silu_mul_bwd(const void* dh, const void* a, const void* b, void* da, void* db, DType t, int64_t n,
+                  hipStream_t s);
+
+// ---- cross entropy (csrc/ops/xent.hip) ----
+void xent_fwd(const void* z, DType t, const int64_t* tgt, float* loss, float* lse, int64_t M, int64_t V,
+              hipStream_t s);
+void xent_bwd(const float* g, const void* z, DType t, const int64_t* tgt, const float* lse, void* dz, float mult,
+              int64_t M, int64_t V, hipStream_t s);
+
+// ---- multi-tensor ops (csrc/ops/multi_tensor.hip) ----
+struct TensorTable {
+  // device arrays, n entries each
+  const int64_t* ptrs;        // [n * nptr] pointers as int64
+  const int64_t* chunk_base;  // [n + 1] prefix sum of chunks per tensor
+  const int64_t* numel;       // [n]
+  int n;
+  int64_t total_chunks;
+};
+constexpr int64_t kMTChunk = 32768;  // elements per workgroup chunk
+
+// scalars are rounded to fp32 from double exactly like the reference's Python-float * fp32-tensor ops
+void adamw_step(const TensorTable& tt, DType grad_t, float beta1, float beta2, float one_minus_beta1,
+                float one_minus_beta2, float eps, float lr_wd, float alpha_t, hipStream_t s);
+void multi_tensor_sumsq(const TensorTable& tt, DType t, float* partials, hipStream_t s);
+void finalize_l2norm(const float* partials, int64_t n, float* out, hipStream_t s);
+void multi_tensor_scale(const TensorTable& tt, DType t, const float* scale, hipStream_t s);
+
+// ---- FlashAttention-2 (csrc/flash_attn/) ----
+struct AttnParams {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  float* lse;  // (B, H, Nq) contiguous
+  // element strides for batch, head, seq (last dim contiguous)
+  int64_t q_sb, q_sh, q_sn;
+  int64_t k_sb, k_sh, k_sn;
+  int64_t v_sb, v_sh, v_sn;
+  int64_t o_sb, o_sh, o_sn;
+  int B, H, Nq, Nk, D;
+  float scale;
+  bool causal;
+};
+
+struct AttnBwdParams {
+  AttnParams f;  // q,k,v,o,lse + strides (o is read)
+  const void* dout;
+  int64_t do_sb, do_sh, do_sn;
+  void* dq;
+  void* dk;
+  void* dv;
+  int64_t dq_sb, dq_sh, dq_sn;
+  int64_t dk_sb, dk_sh, dk_sn;
+  int64_t dv_sb, dv_sh, dv_sn;
+  float* delta;  // (B, H, Nq) workspace
+};
+
+void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s);
+void flash_attn_bwd(const AttnBwdParams& p, DType t, hipStream_t s);
+
+}  // namespace cs336

@@ -1,0 +1,236 @@
+// RMSNorm forward/backward for MI355X (gfx950).
+//
+// Semantics: reference cs336-basics/cs336_basics/model.py:101-107 — y = w * (x * rsqrt(mean(x^2)+eps))
+// computed in fp32, stored in the requested output dtype (bf16 under autocast: the next op is a
+// bf16 GEMM, so the separate cast kernel of the eager path disappears).
+//
+// Layout: one wave64 per row, 4 rows per 256-thread workgroup. The row is read ONCE into
+// registers (NV float4 per lane, NV chosen at dispatch from H), reduced with wave shuffles, and
+// written from registers: 1 read + 1 write of the activation, which is the HBM floor.
+// Backward: each wave walks a strided set of rows, producing dx per row and accumulating its dw
+// partial in registers; partials (one per wave) go to a workspace that a column-tiled kernel
+// reduces (deterministic, no float atomics).
+#include "cs336/kernels.h"
+
+namespace cs336 {
+namespace {
+
+template <typename TX, typename TW, typename TY, int NV>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const typename Elem<TX>::storage* __restrict__ x,
+                                                          const typename Elem<TW>::storage* __restrict__ w,
+                                                          typename Elem<TY>::storage* __restrict__ y,
+                                                          float* __restrict__ rstd, int64_t M, int H, float eps) {
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  if (row >= M) return;
+  const int H4 = H >> 2;
+  const auto* xr = x + row * H;
+  float4 v[NV];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = lane + kWave * k;
+    if (i < H4) {
+      v[k] = load4<TX>(xr + 4 * i);
+      ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+    } else {
+      v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)H + eps);
+  if (lane == 0) rstd[row] = r;
+  auto* yr = y + row * H;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = lane + kWave * k;
+    if (i < H4) {
+      const float4 wv = load4<TW>(w + 4 * i);
+      float4 o;
+      o.x = wv.x * (v[k].x * r);
+      o.y = wv.y * (v[k].y * r);
+      o.z = wv.z * (v[k].z * r);
+      o.w = wv.w * (v[k].w * r);
+      store4<TY>(yr + 4 * i, o);
+    }
+  }
+}
+
+template <typename TDY, typename TX, typename TW, int NV>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const typename Elem<TDY>::storage* __restrict__ dy,
+                                                          const typename Elem<TX>::storage* __restrict__ x,
+                                                          const typename Elem<TW>::storage* __restrict__ w,
+                                                          const float* __restrict__ rstd,
+                                                          typename Elem<TX>::storage* __restrict__ dx,
+                                                          float* __restrict__ ws, int64_t M, int H) {
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int H4 = H >> 2;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
+  float4 wv[NV], dwp[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = lane + kWave * k;
+    wv[k] = i < H4 ? load4<TW>(w + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    dwp[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float invH = 1.f / (float)H;
+  for (int64_t row = gw; row < M; row += nw) {
+    const auto* xr = x + row * H;
+    const auto* dyr = dy + row * H;
+    const float r = rstd[row];
+    float4 xv[NV], gv[NV];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int i = lane + kWave * k;
+      if (i < H4) {
+        xv[k] = load4<TX>(xr + 4 * i);
+        gv[k] = load4<TDY>(dyr + 4 * i);
+        dot += wv[k].x * gv[k].x * xv[k].x + wv[k].y * gv[k].y * xv[k].y + wv[k].z * gv[k].z * xv[k].z +
+               wv[k].w * gv[k].w * xv[k].w;
+      } else {
+        xv[k] = gv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    dot = wave_sum(dot);
+    const float c = r * r * r * invH * dot;
+    auto* dxr = dx + row * H;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int i = lane + kWave * k;
+      if (i < H4) {
+        float4 o;
+        o.x = r * wv[k].x * gv[k].x - c * xv[k].x;
+        o.y = r * wv[k].y * gv[k].y - c * xv[k].y;
+        o.z = r * wv[k].z * gv[k].z - c * xv[k].z;
+        o.w = r * wv[k].w * gv[k].w - c * xv[k].w;
+        store4<TX>(dxr + 4 * i, o);
+        dwp[k].x += gv[k].x * xv[k].x * r;
+        dwp[k].y += gv[k].y * xv[k].y * r;
+        dwp[k].z += gv[k].z * xv[k].z * r;
+        dwp[k].w += gv[k].w * xv[k].w * r;
+      }
+    }
+  }
+  // fold the 4 waves' dw partials through LDS (one partial row per workgroup, in wave order so the
+  // result is deterministic), then workgroup partials are reduced by colsum_kernel
+  extern __shared__ __attribute__((aligned(16))) float red[];  // H floats
+  for (int wv_ = 0; wv_ < 4; ++wv_) {
+    if (wave == wv_) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int i = lane + kWave * k;
+        if (i < H4) {
+          float4* rp = reinterpret_cast<float4*>(red + 4 * i);
+          if (wv_ == 0) {
+            *rp = dwp[k];
+          } else {
+            float4 a = *rp;
+            a.x += dwp[k].x; a.y += dwp[k].y; a.z += dwp[k].z; a.w += dwp[k].w;
+            *rp = a;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* wr = ws + (int64_t)blockIdx.x * H;
+  for (int i = threadIdx.x; i < H4; i += 256) reinterpret_cast<float4*>(wr)[i] = reinterpret_cast<float4*>(red)[i];
+}
+
+// out[s][j] = sum over partial rows p in split s of ws[p][j]; grid (col tiles of 256, splits)
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ ws, float* __restrict__ out, int P,
+                                                     int H) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int per = (P + S - 1) / S;
+  const int p0 = s * per, p1 = min(P, p0 + per);
+  float acc = 0.f;
+  if (j < H)
+    for (int p = p0; p < p1; ++p) acc += ws[(int64_t)p * H + j];
+  if (j < H) out[(int64_t)s * H + j] = acc;
+}
+
+template <int NV, typename F>
+void dispatch_nv(int H, F&& f) {
+  (void)NV;
+  const int per_lane = (H / 4 + kWave - 1) / kWave;
+  if (per_lane <= 2) f(std::integral_constant<int, 2>{});
+  else if (per_lane <= 4) f(std::integral_constant<int, 4>{});
+  else if (per_lane <= 8) f(std::integral_constant<int, 8>{});
+  else if (per_lane <= 16) f(std::integral_constant<int, 16>{});
+  else f(std::integral_constant<int, 32>{});
+}
+
+template <typename F>
+void dispatch_type(DType t, F&& f) {
+  switch (t) {
+    case DType::F32: f(float{}); break;
+    case DType::BF16: f(BF16{}); break;
+    case DType::F16: f(F16{}); break;
+  }
+}
+
+}  // namespace
+
+void rmsnorm_fwd(const void* x, DType xt, const void* w, DType wt, void* y, DType yt, float* rstd, int64_t M,
+                 int64_t H, float eps, hipStream_t s) {
+  const dim3 grid((unsigned)((M + 3) / 4)), block(256);
+  dispatch_nv<0>((int)H, [&](auto nv) {
+    constexpr int NV = decltype(nv)::value;
+    dispatch_type(xt, [&](auto tx) {
+      using TX = decltype(tx);
+      dispatch_type(wt, [&](auto tw) {
+        using TW = decltype(tw);
+        dispatch_type(yt, [&](auto ty) {
+          using TY = decltype(ty);
+          hipLaunchKernelGGL((rmsnorm_fwd_kernel<TX, TW, TY, NV>), grid, block, 0, s,
+                             (const typename Elem<TX>::storage*)x, (const typename Elem<TW>::storage*)w,
+                             (typename Elem<TY>::storage*)y, rstd, M, (int)H, eps);
+        });
+      });
+    });
+  });
+}
+
+// ~2 rows per wave: 4 waves x 2 rows per workgroup keeps ~16 waves/CU streaming (the row loop is
+// latency-bound at low occupancy), capped so the partial-row workspace stays small.
+static int bwd_blocks(int64_t M) {
+  int64_t nb = (M + 7) / 8;
+  return (int)(nb < 4096 ? (nb > 0 ? nb : 1) : 4096);
+}
+constexpr int kColSplits = 32;
+
+int rmsnorm_bwd_workspace_rows(int64_t M, int64_t H) {
+  (void)H;
+  return bwd_blocks(M) + kColSplits;  // rows of H floats: workgroup partials + split sums
+}
+
+void rmsnorm_bwd(const void* dy, DType dyt, const void* x, DType xt, const void* w, DType wt, const float* rstd,
+                 void* dx, float* dw, float* workspace, int64_t M, int64_t H, hipStream_t s) {
+  const int nb = bwd_blocks(M);
+  const size_t lds = (size_t)H * sizeof(float);
+  dispatch_nv<0>((int)H, [&](auto nv) {
+    constexpr int NV = decltype(nv)::value;
+    dispatch_type(dyt, [&](auto tdy) {
+      using TDY = decltype(tdy);
+      dispatch_type(xt, [&](auto tx) {
+        using TX = decltype(tx);
+        dispatch_type(wt, [&](auto tw) {
+          using TW = decltype(tw);
+          hipLaunchKernelGGL((rmsnorm_bwd_kernel<TDY, TX, TW, NV>), dim3(nb), dim3(256), lds, s,
+                             (const typename Elem<TDY>::storage*)dy, (const typename Elem<TX>::storage*)x,
+                             (const typename Elem<TW>::storage*)w, rstd, (typename Elem<TX>::storage*)dx, workspace,
+                             M, (int)H);
+        });
+      });
+    });
+  });
+  float* split = workspace + (int64_t)nb * H;
+  const unsigned ct = (unsigned)((H + 255) / 256);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ct, kColSplits), dim3(256), 0, s, workspace, split, nb, (int)H);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ct, 1), dim3(256), 0, s, split, dw, kColSplits, (int)H);
+}
+
+}  // namespace cs336
