@@ -46,7 +46,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="xl")
     ap.add_argument("--ctx", type=int, default=512)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("CS336_BENCH_BATCH", 16)), help="per-GPU batch")
+    # 24 x 512 = 12288 tokens per GPU: the best hipBLASLt shapes for this model on MI355X (measured
+    # 16 -> 53.3k, 24 -> 59.2k, 32 -> 55.7k tok/s on 1 GPU; scripts/gemm_bench.py explains why)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("CS336_BENCH_BATCH", 24)), help="per-GPU batch")
     ap.add_argument("--vocab", type=int, default=10000)
     ap.add_argument("--ddp", default="bucketed", choices=["bucketed", "individual", "flat", "naive"])
     ap.add_argument("--bucket-mb", type=float, default=None)
@@ -56,7 +58,40 @@ def parse(argv=None):
     ap.add_argument("--clip", type=float, default=0.0, help="global grad-norm clip (0 = off, as the reference bench)")
     ap.add_argument("--backend", default=os.environ.get("CS336_BACKEND", "auto"))
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--no-shadows", action="store_true", help="autocast re-casts weights every forward (A/B)")
+    ap.add_argument("--no-fused-layout", action="store_true", help="separate q/k/v and w1/w3 GEMMs (A/B)")
+    ap.add_argument(
+        "--tunableop",
+        default="auto",
+        choices=["auto", "off", "use", "tune"],
+        help="PyTorch TunableOp GEMM selection: use = load committed hipBLASLt/rocBLAS picks, tune = re-tune and save",
+    )
     return ap.parse_args(argv)
+
+
+def setup_tunableop(mode: str, rank: int) -> str | None:
+    """Per-shape GEMM solution selection (hipBLASLt vs rocBLAS candidates), tuned once on MI355X and
+    committed under cs336_systems/tuning/ so every fresh box replays the same picks."""
+    from cs336_systems.tuning import tunableop_file
+
+    path = tunableop_file()
+    if mode == "auto":
+        mode = "use" if os.path.exists(path) else "off"
+    if mode == "off":
+        return None
+    import torch.cuda.tunable as tunable
+
+    tunable.enable(True)
+    tunable.set_max_tuning_duration(50)
+    tunable.set_max_tuning_iterations(60)
+    if mode == "tune":
+        tunable.tuning_enable(True)
+        tunable.set_filename(path + (f".rank{rank}" if rank else ""))
+    else:
+        tunable.tuning_enable(False)
+        tunable.read_file(path)
+    log(f"TunableOp: {mode} ({path})")
+    return mode
 
 
 def main(argv=None):
@@ -78,13 +113,15 @@ def main(argv=None):
         device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
         if device.type == "cuda":
             torch.cuda.set_device(device)
+    tmode = None
     if device.type == "cuda":
         assert ops.ext_available(), ops.load_error()
         torch.backends.cuda.matmul.allow_tf32 = False
+        tmode = setup_tunableop(args.tunableop, rank)
 
     torch.manual_seed(1234)
     t0 = time.time()
-    model = build_model(args.model, args.ctx, vocab_size=args.vocab, device=device)
+    model = build_model(args.model, args.ctx, vocab_size=args.vocab, device=device, fused_layout=not args.no_fused_layout)
     n_params = sum(p.numel() for p in model.parameters())
     log(f"built {args.model}: {n_params / 1e9:.3f} B params in {time.time() - t0:.1f}s on {device}")
 
@@ -93,15 +130,17 @@ def main(argv=None):
         ddp_model = wrap_ddp(model, args.ddp, bucket_size_mb=bucket)
     else:
         ddp_model = model
+    amp = args.dtype == "bf16" and device.type == "cuda"
+    okw = dict(lr=args.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01)
     if args.sharded and world > 1:
-        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, lr=args.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01)
+        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, **okw)
     else:
-        opt = ops.FusedAdamW(model.parameters(), lr=args.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01)
+        # bf16 compute-weight shadows written by the AdamW kernel (models/fused.py)
+        opt = ops.FusedAdamW(model.parameters(), bf16_shadows=amp and not args.no_shadows, **okw)
 
     gen = torch.Generator(device=device)
     gen.manual_seed(1000 + rank)
     batches = [synthetic_batch(args.batch, args.ctx, args.vocab, device, gen) for _ in range(4)]
-    amp = args.dtype == "bf16" and device.type == "cuda"
 
     def zero_grads():
         if hasattr(ddp_model, "zero_grad") and world > 1 and args.ddp in ("bucketed", "flat"):
@@ -187,6 +226,11 @@ def main(argv=None):
         "peak_mem_gib": round(peak_gib, 2),
         "final_loss": round(last_loss, 4),
     }
+    out["config"]["gemm_selection"] = f"tunableop:{tmode}" if tmode else "hipblaslt default"
+    if tmode == "tune" and rank == 0:
+        import torch.cuda.tunable as tunable
+
+        log(f"TunableOp results are written to {tunable.get_filename()} at exit")
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

@@ -16,10 +16,12 @@ from .transformer import (
 )
 
 
-def build_model(size: str, context_length: int, vocab_size: int = DEFAULT_VOCAB, rope_theta: float = DEFAULT_THETA, device=None, dtype=None):
+def build_model(size: str, context_length: int, vocab_size: int = DEFAULT_VOCAB, rope_theta: float = DEFAULT_THETA, device=None, dtype=None, fused_layout: bool = True):
     """Construct a :class:`BasicsTransformerLM` of a registry size directly on ``device``."""
     cfg = get_model_config(size)
-    return BasicsTransformerLM(vocab_size=vocab_size, context_length=context_length, rope_theta=rope_theta, device=device, dtype=dtype, **cfg)
+    return BasicsTransformerLM(
+        vocab_size=vocab_size, context_length=context_length, rope_theta=rope_theta, device=device, dtype=dtype, fused_layout=fused_layout, **cfg
+    )
 
 
 __all__ = [

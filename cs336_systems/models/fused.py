@@ -1,0 +1,256 @@
+"""Fused weight layout and mixed-precision GEMM path for MI355X.
+
+Three ideas, all invisible to the state dict (parameter names/shapes are the reference's):
+
+1. **Grouped parameters.** ``q_proj/k_proj/v_proj`` and ``w1/w3`` keep their own ``nn.Parameter``
+   objects, but their storage is re-allocated as consecutive row blocks of ONE tensor
+   (:func:`group_params_`). The forward then runs a single GEMM per group (N = 3·d_model for QKV,
+   2·d_ff for W1|W3) instead of three/two narrow ones — the d×d projections are the least
+   efficient hipBLASLt shapes of the model (their dW has only ~40 output tiles for 256 CUs).
+2. **bf16 compute-weight shadows.** A bf16 copy of every weight, laid out like the fp32 masters
+   (groups stay contiguous), is written by the fused AdamW kernel in the same pass as the update
+   (+2 B/param) instead of autocast re-casting all 2 B fp32 weights every forward (6 B/param in
+   separate kernels). Shadows are used only while ``p._version`` matches the version recorded when
+   they were written, so any out-of-band change of a master weight falls back to casting.
+3. **fp32 weight gradients straight from the GEMM.** ``dW = dYᵀ X`` is computed by hipBLASLt with
+   bf16 inputs and an fp32 output (``aten::mm.dtype``), so there is no bf16→fp32 cast kernel per
+   weight in backward.
+
+:class:`AttentionCore` and :class:`SwiGLUGate` consume the fused projection outputs in place
+(strided views: no split/cat copies) and produce the fused dY for the grouped GEMM's backward.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..ops._ext import ops as _hip
+
+_SHADOW = "_cs336_bf16"
+_SHADOW_VER = "_cs336_bf16_ver"
+
+
+# ------------------------------------------------------------------------------------------
+# grouped storage
+# ------------------------------------------------------------------------------------------
+@torch.no_grad()
+def group_params_(params: list[nn.Parameter]) -> torch.Tensor:
+    """Re-home ``params`` (2-D, same width/dtype/device) as consecutive row blocks of one tensor."""
+    d_in = params[0].shape[1]
+    rows = sum(p.shape[0] for p in params)
+    base = torch.empty(rows, d_in, dtype=params[0].dtype, device=params[0].device)
+    off = 0
+    for p in params:
+        n = p.shape[0]
+        base[off : off + n].copy_(p.data)
+        p.data = base[off : off + n]
+        off += n
+    return base
+
+
+def _adjacent_rows(ts: list[torch.Tensor]) -> torch.Tensor | None:
+    """If ``ts`` are row-adjacent contiguous blocks of one storage, return the combined 2-D view."""
+    t0 = ts[0]
+    if t0.dim() != 2 or not t0.is_contiguous():
+        return None
+    d_in = t0.shape[1]
+    ptr = t0.untyped_storage().data_ptr()
+    off = t0.storage_offset()
+    rows = 0
+    for t in ts:
+        if (
+            t.dim() != 2
+            or t.shape[1] != d_in
+            or not t.is_contiguous()
+            or t.dtype != t0.dtype
+            or t.untyped_storage().data_ptr() != ptr
+            or t.storage_offset() != off + rows * d_in
+        ):
+            return None
+        rows += t.shape[0]
+    return torch.as_strided(t0.detach(), (rows, d_in), (d_in, 1), off)
+
+
+def grouped_view(params: list[nn.Parameter]) -> torch.Tensor | None:
+    return _adjacent_rows(list(params))
+
+
+# ------------------------------------------------------------------------------------------
+# bf16 shadows
+# ------------------------------------------------------------------------------------------
+def has_shadow(p: torch.Tensor) -> bool:
+    return getattr(p, _SHADOW, None) is not None
+
+
+def shadow_valid(p: torch.Tensor) -> bool:
+    return getattr(p, _SHADOW, None) is not None and getattr(p, _SHADOW_VER, None) == p._version
+
+
+def get_shadow(p: torch.Tensor) -> torch.Tensor | None:
+    return getattr(p, _SHADOW, None)
+
+
+def mark_shadow_synced(p: torch.Tensor) -> None:
+    setattr(p, _SHADOW_VER, p._version)
+
+
+@torch.no_grad()
+def attach_bf16_shadows(module_or_params) -> int:
+    """Allocate bf16 shadows for every 2-D fp32 GPU weight (grouped weights get one contiguous
+    shadow per group, mirroring the master layout) and fill them. Returns #params."""
+    src = module_or_params.parameters() if isinstance(module_or_params, nn.Module) else module_or_params
+    params = [p for p in src if p.dim() == 2 and p.dtype == torch.float32 and p.is_cuda and not has_shadow(p)]
+    by_storage: dict[int, list[nn.Parameter]] = {}
+    for p in params:
+        by_storage.setdefault(p.untyped_storage().data_ptr(), []).append(p)
+    for group in by_storage.values():
+        group.sort(key=lambda t: t.storage_offset())
+        base = group[0]
+        st_numel = base.untyped_storage().nbytes() // base.element_size()
+        shadow_base = torch.empty(st_numel, dtype=torch.bfloat16, device=base.device)
+        for p in group:
+            setattr(p, _SHADOW, torch.as_strided(shadow_base, p.shape, p.stride(), p.storage_offset()))
+    refresh_bf16_shadows(params)
+    return len(params)
+
+
+@torch.no_grad()
+def refresh_bf16_shadows(params) -> None:
+    ps = [p for p in params if has_shadow(p)]
+    if not ps:
+        return
+    if ops.ext_available() and all(p.is_contiguous() for p in ps):
+        _hip().multi_tensor_cast_bf16([p.data for p in ps], [get_shadow(p) for p in ps])
+    else:
+        for p in ps:
+            get_shadow(p).copy_(p.data)
+    for p in ps:
+        mark_shadow_synced(p)
+
+
+def compute_weight(params: list[nn.Parameter], dtype: torch.dtype) -> torch.Tensor:
+    """The (rows, d_in) weight in ``dtype`` for a group (or single) of params: the shadow view when
+    valid, else one cast of the (grouped) master view, else a concatenation (ungrouped fallback)."""
+    if dtype == torch.bfloat16 and all(shadow_valid(p) for p in params):
+        v = _adjacent_rows([get_shadow(p) for p in params])
+        if v is not None:
+            return v
+    g = grouped_view(params) if len(params) > 1 else params[0].detach()
+    if g is None:
+        g = torch.cat([p.detach() for p in params], 0)
+    return g if g.dtype == dtype else g.to(dtype)
+
+
+# ------------------------------------------------------------------------------------------
+# fused linear
+# ------------------------------------------------------------------------------------------
+def _mm_fp32_out(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ b with an fp32 result: bf16 x bf16 -> fp32 in one hipBLASLt call when available."""
+    if a.dtype == torch.bfloat16 and a.is_cuda:
+        try:
+            return torch.mm(a, b, out_dtype=torch.float32)
+        except (TypeError, RuntimeError):
+            pass
+    return torch.mm(a, b).float()
+
+
+class FusedLinearFn(torch.autograd.Function):
+    """y = x @ [W_0; W_1; ...]^T for a group of weights with one GEMM; grads come back as row
+    views of one fp32 dW."""
+
+    @staticmethod
+    def forward(ctx, x, *weights):
+        amp = torch.is_autocast_enabled("cuda") and x.is_cuda
+        cdt = torch.get_autocast_dtype("cuda") if amp else weights[0].dtype
+        w = compute_weight(list(weights), cdt)
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.dtype != cdt:
+            x2 = x2.to(cdt)
+        y = torch.mm(x2, w.t())
+        ctx.save_for_backward(x2, w)
+        ctx.x_shape = x.shape
+        ctx.x_dtype = x.dtype
+        ctx.rows = [p.shape[0] for p in weights]
+        ctx.wdtype = [p.dtype for p in weights]
+        return y.view(*x.shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if dy2.dtype != w.dtype:
+            dy2 = dy2.to(w.dtype)
+        dx = dw_parts = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy2, w).view(ctx.x_shape)
+            if dx.dtype != ctx.x_dtype:
+                dx = dx.to(ctx.x_dtype)
+        if any(ctx.needs_input_grad[1:]):
+            dw = _mm_fp32_out(dy2.t(), x2)
+            dw_parts = list(torch.split(dw, ctx.rows, 0))
+            dw_parts = [g if g.dtype == dt else g.to(dt) for g, dt in zip(dw_parts, ctx.wdtype)]
+        return (dx, *(dw_parts if dw_parts is not None else [None] * len(ctx.rows)))
+
+
+def fused_linear(x: torch.Tensor, *weights: nn.Parameter) -> torch.Tensor:
+    return FusedLinearFn.apply(x, *weights)
+
+
+# ------------------------------------------------------------------------------------------
+# attention core on the fused QKV layout
+# ------------------------------------------------------------------------------------------
+class AttentionCore(torch.autograd.Function):
+    """qkv (B, N, 3*H*dk) -> RoPE(q), RoPE(k) -> causal FA2 -> o as a (B, H, N, dk) view of
+    (B, N, H, dk) memory. Backward returns d(qkv) in the same fused layout: FA2 writes dq, dk, dv
+    straight into the three slices of one buffer, then the inverse rotation runs in place."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, pos, H):
+        B, N, three_d = qkv.shape
+        dk = three_d // (3 * H)
+        y5 = qkv.view(B, N, 3, H, dk)
+        q_in = y5[:, :, 0].transpose(1, 2)
+        k_in = y5[:, :, 1].transpose(1, 2)
+        v = y5[:, :, 2].transpose(1, 2)
+        hip = _hip()
+        q = hip.rope(q_in, cos, sin, pos, False)
+        k = hip.rope(k_in, cos, sin, pos, False)
+        scale = dk**-0.5
+        o, lse = hip.fa_fwd(q, k, v, True, scale)
+        ctx.save_for_backward(q, k, qkv, o, lse, cos, sin, pos)
+        ctx.H, ctx.scale = H, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, qkv, o, lse, cos, sin, pos = ctx.saved_tensors
+        B, N, three_d = qkv.shape
+        H = ctx.H
+        dk = three_d // (3 * H)
+        v = qkv.view(B, N, 3, H, dk)[:, :, 2].transpose(1, 2)
+        dqkv = torch.empty_like(qkv)
+        d5 = dqkv.view(B, N, 3, H, dk)
+        dq, dkk, dv = (d5[:, :, i].transpose(1, 2) for i in range(3))
+        if do.stride(-1) != 1:
+            do = do.contiguous()
+        hip = _hip()
+        hip.fa_bwd_into(do, q, k, v, o, lse, True, ctx.scale, dq, dkk, dv)
+        hip.rope_into(dq, cos, sin, pos, True, dq)
+        hip.rope_into(dkk, cos, sin, pos, True, dkk)
+        return dqkv, None, None, None, None
+
+
+class SwiGLUGate(torch.autograd.Function):
+    """h = silu(a) * b with [a | b] = y the fused W1|W3 output; backward emits dy = [da | db]."""
+
+    @staticmethod
+    def forward(ctx, y):
+        ctx.save_for_backward(y)
+        return _hip().swiglu_fused_fwd(y)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (y,) = ctx.saved_tensors
+        return _hip().swiglu_fused_bwd(dh.contiguous(), y)

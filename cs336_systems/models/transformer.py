@@ -29,7 +29,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops.rope import _normalize_pos
 from ..utils.profiling import annotate
+from . import fused
 
 logger = logging.getLogger(__name__)
 
@@ -63,6 +65,8 @@ class Linear(nn.Module):
         self.weight = nn.Parameter(_trunc_normal((d_out, d_in), std, device, dtype), requires_grad=True)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:
+            return fused.fused_linear(x, self.weight)
         return F.linear(x, self.weight)
 
     def extra_repr(self):
@@ -142,7 +146,14 @@ class SwiGLU(nn.Module):
         self.w2 = Linear(d_ff, d_model, device, dtype)
         self.w3 = Linear(d_model, d_ff, device, dtype)
 
+    def group_(self) -> None:
+        """Store w1 and w3 as one (2*d_ff, d_model) block so the gate projections are one GEMM."""
+        fused.group_params_([self.w1.weight, self.w3.weight])
+
     def forward(self, x):
+        if x.is_cuda and ops.use_hip(x) and fused.grouped_view([self.w1.weight, self.w3.weight]) is not None:
+            y = fused.fused_linear(x, self.w1.weight, self.w3.weight)  # [a | b], (..., 2*d_ff)
+            return self.w2(fused.SwiGLUGate.apply(y))
         return self.w2(ops.silu_mul(self.w1(x), self.w3(x)))
 
 
@@ -177,12 +188,40 @@ class CausalMultiHeadSelfAttention(nn.Module):
         self.output_proj = Linear(num_heads * self.d_v, d_model, device, dtype)
         self.positional_encoder = positional_encoder
 
+    def group_(self) -> None:
+        """Store q/k/v projections as one (3*d_model, d_model) block (one QKV GEMM)."""
+        fused.group_params_([self.q_proj.weight, self.k_proj.weight, self.v_proj.weight])
+
+    def _fused_path(self, x3, pos, B, N):
+        """GPU path over the grouped QKV weight: one GEMM -> RoPE + FA2 on strided views -> o."""
+        w = [self.q_proj.weight, self.k_proj.weight, self.v_proj.weight]
+        if _ATTN_IMPL == "naive" or not ops.use_hip(x3) or self.d_k not in (32, 64, 128):
+            return None
+        if fused.grouped_view(w) is None:
+            return None
+        p = _normalize_pos(pos, B, N)
+        if isinstance(p, str):
+            return None
+        cos, sin = self.positional_encoder.cos.float().contiguous(), self.positional_encoder.sin.float().contiguous()
+        if p is None and N > cos.shape[0]:
+            return None
+        with annotate("qkv_proj"):
+            qkv = fused.fused_linear(x3, *w)  # (B, N, 3*H*dk)
+        with annotate("attention"):
+            return fused.AttentionCore.apply(qkv, cos, sin, p, self.num_heads)
+
     def forward(self, x: torch.Tensor, token_positions: torch.Tensor | None = None) -> torch.Tensor:
         *b, N, d_model = x.shape
         assert d_model == self.d_model
         B = int(math.prod(b)) if b else 1
         H, dk = self.num_heads, self.d_k
         x3 = x.reshape(B, N, d_model)
+        if x.is_cuda:
+            o = self._fused_path(x3, token_positions, B, N)
+            if o is not None:
+                o = o.transpose(1, 2).reshape(*b, N, H * dk) if b else o.transpose(1, 2).reshape(N, H * dk)
+                with annotate("out_proj"):
+                    return self.output_proj(o)
         # (B, N, H, dk) memory, viewed as (B, H, N, dk): no transpose copies on the GPU path
         with annotate("qkv_proj"):
             q = self.q_proj(x3).view(B, N, H, dk).transpose(1, 2)
@@ -244,6 +283,7 @@ class BasicsTransformerLM(nn.Module):
         *,
         device=None,
         dtype=None,
+        fused_layout: bool = True,
     ):
         self.config = dict(
             vocab_size=vocab_size,
@@ -255,6 +295,7 @@ class BasicsTransformerLM(nn.Module):
             rope_theta=rope_theta,
         )
         super().__init__()
+        self._fused_layout = fused_layout
         self.vocab_size = vocab_size
         self.context_length = context_length
         self.d_model = d_model
@@ -265,7 +306,23 @@ class BasicsTransformerLM(nn.Module):
         )
         self.ln_final = RMSNorm(d_model, device=device, dtype=dtype)
         self.lm_head = Linear(d_model, vocab_size, device, dtype)
+        if fused_layout:
+            self.regroup_()
         logger.info(f"number of non-embedding parameters: {self.get_num_params() / 1e6:.2f}M")
+
+    def regroup_(self) -> "BasicsTransformerLM":
+        """(Re)establish the grouped QKV / W1|W3 storage (e.g. after ``.to(device)``, which gives
+        every parameter its own storage). Parameter objects, names and values are unchanged."""
+        for layer in self.layers:
+            layer.attn.group_()
+            layer.ffn.group_()
+        return self
+
+    def _apply(self, fn, recurse=True):
+        out = super()._apply(fn, recurse)
+        if getattr(self, "_fused_layout", False) and hasattr(self, "layers"):
+            self.regroup_()
+        return out
 
     def get_num_params(self, non_embedding: bool = True) -> int:
         n = sum(p.numel() for p in self.parameters())

@@ -62,3 +62,28 @@ def _xent_bwd(g, z, t, lse, mult):
 @register_fake("cs336::multi_tensor_l2norm")
 def _l2(ts):
     return ts[0].new_empty((), dtype=torch.float32)
+
+
+@register_fake("cs336::fa_bwd_into")
+def _fa_bwd_into(do, q, k, v, o, lse, causal, scale, dq, dk, dv):
+    return None
+
+
+@register_fake("cs336::rope_into")
+def _rope_into(x, cos, sin, pos, inverse, out):
+    return None
+
+
+@register_fake("cs336::swiglu_fused_fwd")
+def _swiglu_fused_fwd(y):
+    return y.new_empty((*y.shape[:-1], y.shape[-1] // 2))
+
+
+@register_fake("cs336::swiglu_fused_bwd")
+def _swiglu_fused_bwd(dh, y):
+    return torch.empty_like(y)
+
+
+@register_fake("cs336::multi_tensor_cast_bf16")
+def _cast_bf16(src, dst):
+    return None

@@ -46,7 +46,11 @@ class FusedAdamW(torch.optim.Optimizer):
         betas: tuple[float, float] = (0.9, 0.999),
         eps: float = 1e-8,
         weight_decay: float = 0.01,
+        bf16_shadows: bool = False,
     ):
+        """``bf16_shadows=True``: every 2-D fp32 GPU weight gets a bf16 copy that the update kernel
+        rewrites in the same pass; the model's GEMMs read it instead of re-casting under autocast
+        (``cs336_systems/models/fused.py``)."""
         if not 0.0 <= lr:
             raise ValueError(f"Invalid learning rate: {lr}")
         if not 0.0 <= eps:
@@ -56,6 +60,10 @@ class FusedAdamW(torch.optim.Optimizer):
         if not 0.0 <= betas[1] < 1.0:
             raise ValueError(f"Invalid beta parameter at index 1: {betas[1]}")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        if bf16_shadows:
+            from ..models.fused import attach_bf16_shadows
+
+            attach_bf16_shadows([p for g in self.param_groups for p in g["params"]])
 
     @torch.no_grad()
     def step(self, closure: Callable | None = None):
@@ -68,8 +76,11 @@ class FusedAdamW(torch.optim.Optimizer):
             beta1, beta2 = group["betas"]
             eps = group["eps"]
             wd = group["weight_decay"]
-            # bucket by (device, dtype, t) so each launch has a single bias correction
-            buckets: dict[tuple, tuple[list, list, list, list]] = {}
+            from ..models.fused import get_shadow, mark_shadow_synced
+
+            # bucket by (device, dtype, t, shadow) so each launch has one bias correction and an
+            # all-or-nothing shadow list
+            buckets: dict[tuple, tuple[list, list, list, list, list]] = {}
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -80,19 +91,26 @@ class FusedAdamW(torch.optim.Optimizer):
                     state["m"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state["v"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state["t"] = 1
-                key = (p.device, p.dtype, p.grad.dtype, state["t"])
-                b = buckets.setdefault(key, ([], [], [], []))
+                sh = get_shadow(p)
+                key = (p.device, p.dtype, p.grad.dtype, state["t"], sh is not None)
+                b = buckets.setdefault(key, ([], [], [], [], []))
                 b[0].append(p)
                 b[1].append(p.grad)
                 b[2].append(state["m"])
                 b[3].append(state["v"])
+                if sh is not None:
+                    b[4].append(sh)
                 state["t"] += 1
-            for (dev, _, _, t), (ps, gs, ms, vs) in buckets.items():
-                if use_hip(ps[0]) and all(x.is_contiguous() for x in ps + gs + ms + vs):
-                    ops().adamw_step(ps, gs, ms, vs, lr, beta1, beta2, eps, wd, t)
+            for (dev, _, _, t, _), (ps, gs, ms, vs, ss) in buckets.items():
+                if use_hip(ps[0]) and all(x.is_contiguous() for x in ps + gs + ms + vs + ss):
+                    ops().adamw_step(ps, gs, ms, vs, ss, lr, beta1, beta2, eps, wd, t)
                 else:
                     for p, g, m, v in zip(ps, gs, ms, vs):
                         adamw_ref_(p, g.to(p.dtype), m, v, lr, beta1, beta2, eps, wd, t)
+                    for p, s in zip(ps, ss):
+                        s.copy_(p)
+                for p in ps if ss else ():
+                    mark_shadow_synced(p)
         return loss
 
 

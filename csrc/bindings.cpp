@@ -90,6 +90,10 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
   return {o, lse};
 }
 
+void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
+                const at::Tensor& dk, const at::Tensor& dv);
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
                                                       const at::Tensor& v, const at::Tensor& out,
                                                       const at::Tensor& lse, bool causal, double scale) {
@@ -104,6 +108,35 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_bwd(const at::Tensor& dout, co
   at::Tensor dq = empty_bnhd_like(q);
   at::Tensor dk = empty_bnhd_like(k);
   at::Tensor dv = empty_bnhd_like(v);
+  fa_bwd_run(dout, q, k, v, out, lse, causal, scale, dq, dk, dv);
+  return {dq, dk, dv};
+}
+
+// backward writing dq/dk/dv into caller-provided (B,H,N,D) strided views (e.g. the three slices of
+// one fused dQKV buffer that feeds the fused QKV-projection GEMM)
+void fa_bwd_into(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                 const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
+                 const at::Tensor& dk, const at::Tensor& dv) {
+  check_bhnd(q, "q");
+  check_bhnd(k, "k");
+  check_bhnd(v, "v");
+  check_bhnd(out, "out");
+  check_bhnd(dout, "dout");
+  check_bhnd(dq, "dq");
+  check_bhnd(dk, "dk");
+  check_bhnd(dv, "dv");
+  TORCH_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "cs336: grad shapes");
+  TORCH_CHECK(dq.scalar_type() == q.scalar_type() && dk.scalar_type() == q.scalar_type() &&
+                  dv.scalar_type() == q.scalar_type() && dout.scalar_type() == q.scalar_type(),
+              "cs336: dtype mismatch");
+  TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == at::kFloat, "cs336: lse must be contiguous fp32");
+  c10::DeviceGuard g(q.device());
+  fa_bwd_run(dout, q, k, v, out, lse, causal, scale, dq, dk, dv);
+}
+
+void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
+                const at::Tensor& dk, const at::Tensor& dv) {
   at::Tensor delta = at::empty({q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
   cs336::AttnBwdParams bp;
   fill_attn(bp.f, q, k, v, out, lse, causal, scale);
@@ -117,7 +150,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_bwd(const at::Tensor& dout, co
   bp.dv_sb = dv.stride(0); bp.dv_sh = dv.stride(1); bp.dv_sn = dv.stride(2);
   bp.delta = delta.data_ptr<float>();
   cs336::flash_attn_bwd(bp, to_dtype(q), stream());
-  return {dq, dk, dv};
 }
 
 // ------------------------------------------------------------------------------------------
@@ -157,15 +189,30 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
 // ------------------------------------------------------------------------------------------
 // RoPE
 // ------------------------------------------------------------------------------------------
+void rope_into(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, const std::optional<at::Tensor>& pos,
+               bool inverse, const at::Tensor& out);
+
 at::Tensor rope(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, const std::optional<at::Tensor>& pos,
                 bool inverse) {
   check_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 4, "cs336: rope x must be (B,H,N,D)");
+  c10::DeviceGuard g(x.device());
+  at::Tensor out = empty_bnhd_like(x);
+  rope_into(x, cos, sin, pos, inverse, out);
+  return out;
+}
+
+// writes into a caller-provided (B,H,N,D) strided view (e.g. a slice of a fused dQKV buffer)
+void rope_into(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, const std::optional<at::Tensor>& pos,
+               bool inverse, const at::Tensor& out) {
+  check_cuda(x, "x");
   TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "cs336: rope x must be (B,H,N,D) with contiguous D");
+  TORCH_CHECK(out.dim() == 4 && out.stride(3) == 1 && out.sizes() == x.sizes() && out.dtype() == x.dtype(),
+              "cs336: rope out must match x with contiguous D");
   TORCH_CHECK(x.size(3) % 4 == 0, "cs336: rope head dim must be a multiple of 4");
   TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.is_contiguous() && sin.is_contiguous(), "cs336: rope cache");
   TORCH_CHECK(cos.size(1) * 2 == x.size(3), "cs336: rope cache width");
   c10::DeviceGuard g(x.device());
-  at::Tensor out = empty_bnhd_like(x);
   const int64_t* pp = nullptr;
   if (pos.has_value() && pos->defined()) {
     TORCH_CHECK(pos->scalar_type() == at::kLong && pos->is_contiguous() && pos->numel() == x.size(0) * x.size(2),
@@ -174,11 +221,11 @@ at::Tensor rope(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& si
   } else {
     TORCH_CHECK(x.size(2) <= cos.size(0), "cs336: sequence longer than the RoPE cache");
   }
-  if (x.numel() == 0) return out;
-  cs336::rope(x.data_ptr(), to_dtype(x), x.stride(0), x.stride(1), x.stride(2), out.data_ptr(), cos.data_ptr<float>(),
-              sin.data_ptr<float>(), pp, (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), inverse,
-              stream());
-  return out;
+  if (x.numel() == 0) return;
+  cs336::RopeArgs ra{x.data_ptr(), x.stride(0), x.stride(1), x.stride(2), out.data_ptr(), out.stride(0), out.stride(1),
+                     out.stride(2)};
+  cs336::rope(ra, to_dtype(x), cos.data_ptr<float>(), sin.data_ptr<float>(), pp, (int)x.size(0), (int)x.size(1),
+              (int)x.size(2), (int)x.size(3), inverse, stream());
 }
 
 // ------------------------------------------------------------------------------------------
@@ -190,7 +237,7 @@ at::Tensor silu_mul_fwd(const at::Tensor& a, const at::Tensor& b) {
               "cs336: silu_mul operands");
   c10::DeviceGuard g(a.device());
   at::Tensor h = at::empty_like(a);
-  cs336::silu_mul_fwd(a.data_ptr(), b.data_ptr(), h.data_ptr(), to_dtype(a), a.numel(), stream());
+  cs336::silu_mul_fwd(a.data_ptr(), b.data_ptr(), h.data_ptr(), to_dtype(a), 1, a.numel(), a.numel(), stream());
   return h;
 }
 
@@ -199,9 +246,35 @@ std::tuple<at::Tensor, at::Tensor> silu_mul_bwd(const at::Tensor& dh, const at::
   TORCH_CHECK(dh.is_contiguous() && dh.sizes() == a.sizes() && dh.dtype() == a.dtype(), "cs336: silu_mul_bwd dh");
   c10::DeviceGuard g(a.device());
   at::Tensor da = at::empty_like(a), db = at::empty_like(b);
-  cs336::silu_mul_bwd(dh.data_ptr(), a.data_ptr(), b.data_ptr(), da.data_ptr(), db.data_ptr(), to_dtype(a), a.numel(),
-                      stream());
+  cs336::silu_mul_bwd(dh.data_ptr(), a.data_ptr(), b.data_ptr(), da.data_ptr(), db.data_ptr(), to_dtype(a), 1,
+                      a.numel(), a.numel(), stream());
   return {da, db};
+}
+
+// fused layout: y = [a | b] of shape (..., 2F) (output of the fused W1|W3 GEMM) -> h (..., F)
+at::Tensor swiglu_fused_fwd(const at::Tensor& y) {
+  check_cuda(y, "y");
+  TORCH_CHECK(y.is_contiguous() && y.size(-1) % 8 == 0, "cs336: swiglu_fused y must be contiguous (..., 2F), F%4==0");
+  c10::DeviceGuard g(y.device());
+  const int64_t F = y.size(-1) / 2, M = y.numel() / y.size(-1);
+  auto sizes = y.sizes().vec();
+  sizes.back() = F;
+  at::Tensor h = at::empty(sizes, y.options());
+  const int64_t es = y.element_size();
+  cs336::silu_mul_fwd(y.data_ptr(), (char*)y.data_ptr() + F * es, h.data_ptr(), to_dtype(y), M, F, 2 * F, stream());
+  return h;
+}
+
+at::Tensor swiglu_fused_bwd(const at::Tensor& dh, const at::Tensor& y) {
+  check_cuda(y, "y");
+  TORCH_CHECK(dh.is_contiguous() && dh.dtype() == y.dtype() && dh.numel() * 2 == y.numel(), "cs336: swiglu_fused_bwd");
+  c10::DeviceGuard g(y.device());
+  const int64_t F = y.size(-1) / 2, M = y.numel() / y.size(-1);
+  at::Tensor dy = at::empty_like(y);
+  const int64_t es = y.element_size();
+  cs336::silu_mul_bwd(dh.data_ptr(), y.data_ptr(), (char*)y.data_ptr() + F * es, dy.data_ptr(),
+                      (char*)dy.data_ptr() + F * es, to_dtype(y), M, F, 2 * F, stream());
+  return dy;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -275,20 +348,32 @@ void check_same_dtype(const std::vector<at::Tensor>& ts, at::ScalarType st, cons
 }
 
 void adamw_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> exp_avg,
-                std::vector<at::Tensor> exp_avg_sq, double lr, double beta1, double beta2, double eps,
-                double weight_decay, int64_t step) {
+                std::vector<at::Tensor> exp_avg_sq, std::vector<at::Tensor> shadows, double lr, double beta1,
+                double beta2, double eps, double weight_decay, int64_t step) {
   if (params.empty()) return;
   check_same_dtype(params, at::kFloat, "params (fp32 master weights)");
   check_same_dtype(exp_avg, at::kFloat, "exp_avg");
   check_same_dtype(exp_avg_sq, at::kFloat, "exp_avg_sq");
   const at::ScalarType gt = grads[0].scalar_type();
   check_same_dtype(grads, gt, "grads");
+  const bool shadow = !shadows.empty();
+  if (shadow) check_same_dtype(shadows, at::kBFloat16, "bf16 shadows");
   c10::DeviceGuard g(params[0].device());
-  HostTable ht = build_table({params, grads, exp_avg, exp_avg_sq});
+  HostTable ht = shadow ? build_table({params, grads, exp_avg, exp_avg_sq, shadows})
+                        : build_table({params, grads, exp_avg, exp_avg_sq});
   // alpha * (sqrt(1 - b2^t) / (1 - b1^t)) in double, as the reference evaluates it in Python
   const double alpha_t = lr * (std::sqrt(1.0 - std::pow(beta2, (double)step)) / (1.0 - std::pow(beta1, (double)step)));
-  cs336::adamw_step(ht.tt, to_dtype(grads[0]), (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2),
-                    (float)eps, (float)(lr * weight_decay), (float)alpha_t, stream());
+  cs336::adamw_step(ht.tt, to_dtype(grads[0]), shadow, (float)beta1, (float)beta2, (float)(1.0 - beta1),
+                    (float)(1.0 - beta2), (float)eps, (float)(lr * weight_decay), (float)alpha_t, stream());
+}
+
+void multi_tensor_cast_bf16(std::vector<at::Tensor> src, std::vector<at::Tensor> dst) {
+  if (src.empty()) return;
+  check_same_dtype(src, at::kFloat, "src");
+  check_same_dtype(dst, at::kBFloat16, "dst");
+  c10::DeviceGuard g(src[0].device());
+  HostTable ht = build_table({src, dst});
+  cs336::multi_tensor_cast_bf16(ht.tt, stream());
 }
 
 at::Tensor multi_tensor_l2norm(std::vector<at::Tensor> tensors) {
@@ -324,13 +409,20 @@ TORCH_LIBRARY(cs336, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, Tensor? pos, bool inverse) -> Tensor");
+  m.def(
+      "fa_bwd_into(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale, "
+      "Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
+  m.def("rope_into(Tensor x, Tensor cos, Tensor sin, Tensor? pos, bool inverse, Tensor(a!) out) -> ()");
+  m.def("swiglu_fused_fwd(Tensor y) -> Tensor");
+  m.def("swiglu_fused_bwd(Tensor dh, Tensor y) -> Tensor");
+  m.def("multi_tensor_cast_bf16(Tensor[] src, Tensor(a!)[] dst) -> ()");
   m.def("silu_mul_fwd(Tensor a, Tensor b) -> Tensor");
   m.def("silu_mul_bwd(Tensor dh, Tensor a, Tensor b) -> (Tensor, Tensor)");
   m.def("xent_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor)");
   m.def("xent_bwd(Tensor g, Tensor logits, Tensor targets, Tensor lse, float mult) -> Tensor");
   m.def(
-      "adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
-      "float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
+      "adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, "
+      "Tensor(d!)[] shadows, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("multi_tensor_l2norm(Tensor[] tensors) -> Tensor");
   m.def("multi_tensor_scale_(Tensor(a!)[] tensors, Tensor scale) -> ()");
 }
@@ -341,6 +433,11 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
   m.impl("rope", &rope);
+  m.impl("fa_bwd_into", &fa_bwd_into);
+  m.impl("rope_into", &rope_into);
+  m.impl("swiglu_fused_fwd", &swiglu_fused_fwd);
+  m.impl("swiglu_fused_bwd", &swiglu_fused_bwd);
+  m.impl("multi_tensor_cast_bf16", &multi_tensor_cast_bf16);
   m.impl("silu_mul_fwd", &silu_mul_fwd);
   m.impl("silu_mul_bwd", &silu_mul_bwd);
   m.impl("xent_fwd", &xent_fwd);

@@ -27,11 +27,14 @@ namespace fa {
 template <typename T, int D, bool CAUSAL>
 __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
-  const AttnParams& p = bp.f;
+  const AttnParams p = bp.f;  // by value: a reference would spill the kernarg struct to scratch
   constexpr bool F32 = std::is_same<T, float>::value;
   constexpr int ES = sizeof(S);
   constexpr int RB = D * ES, CPR = RB / 16, EPC = 16 / ES;
-  constexpr int BM = 128, BN = 64;
+  // D=128 streams 32-key tiles: halves the S^T/dP^T/staging registers so the kernel fits 256
+  // VGPRs without spilling (64-key tiles spilled at occupancy 1)
+  constexpr int BM = 128, BN = D == 128 ? 32 : 64;
+  constexpr int NT = BN / 32;
   constexpr int TILE = BN * RB;
   constexpr int LPT = BN * CPR / 256;
   constexpr int NDT = D / 32;
@@ -99,7 +102,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
         kst[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)key * p.k_sn + ch * EPC);
         vst[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)key * p.v_sn + ch * EPC);
       } else {
-        kst[i] = vst[i] = make_uint4(0, 0, 0, 0);
+        kst[i] = make_uint4(0, 0, 0, 0);
+        vst[i] = make_uint4(0, 0, 0, 0);
       }
     }
   };
@@ -133,9 +137,9 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
     if (active) {
       const char* Ks = smem + buf * 2 * TILE;
       const char* Vs = Ks + TILE;
-      f32x16 s[2], dp[2];
+      f32x16 s[NT], dp[NT];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < NT; ++t) {
         s[t] = zero16();
         dp[t] = zero16();
         if constexpr (F32) {
@@ -164,7 +168,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
       }
       const bool need_mask = (kt0 + BN > p.Nk) || (CAUSAL && kt0 + BN - 1 > qw0);
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float pv = fexp2(fmaf(s[t][r], c2, -lse2));
@@ -178,21 +182,21 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
+          for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r)
               dq[dt] = mma_f32(lds_f1<RB>(Ks, 32 * t + acc_row(r, hh), dt * 32 + l32), s[t][r], dq[dt]);
       } else {
-        typename Mma16<T>::frag pf[2][2];
+        typename Mma16<T>::frag pf[NT][2];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < NT; ++t) {
           pf[t][0] = pack_acc<T>(s[t], 0);
           pf[t][1] = pack_acc<T>(s[t], 1);
         }
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
+          for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2)
               dq[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Ks, 32 * t, s2, dt, lane), pf[t][s2], dq[dt]);
@@ -230,16 +234,18 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
 template <typename T, int D, bool CAUSAL>
 __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
-  const AttnParams& p = bp.f;
+  const AttnParams p = bp.f;  // by value: a reference would spill the kernarg struct to scratch
   constexpr bool F32 = std::is_same<T, float>::value;
   constexpr int ES = sizeof(S);
   constexpr int RB = D * ES, CPR = RB / 16, EPC = 16 / ES;
-  constexpr int BK = 128, BQ = 64;
+  // D=128 streams 32-query tiles (register budget: resident K/V fragments + dK/dV accumulators)
+  constexpr int BK = 128, BQ = D == 128 ? 32 : 64;
+  constexpr int NT = BQ / 32;
   constexpr int TILE = BQ * RB;
   constexpr int BUF = 2 * TILE + 2 * BQ * 4;  // Q, dO images + L2, delta rows
   constexpr int LPT = BQ * CPR / 256;
   constexpr int NDT = D / 32;
-  constexpr bool PREFETCH = D <= 64;
+  constexpr bool PREFETCH = !(F32 && D == 128);
 
   __shared__ __attribute__((aligned(16))) char smem[(PREFETCH ? 2 : 1) * BUF];
 
@@ -295,7 +301,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
         qst[i] = *reinterpret_cast<const uint4*>(Qp + (int64_t)q * p.q_sn + ch * EPC);
         dst[i] = *reinterpret_cast<const uint4*>(dOp + (int64_t)q * bp.do_sn + ch * EPC);
       } else {
-        qst[i] = dst[i] = make_uint4(0, 0, 0, 0);
+        qst[i] = make_uint4(0, 0, 0, 0);
+        dst[i] = make_uint4(0, 0, 0, 0);
       }
     }
     if (tid < BQ) {
@@ -343,9 +350,9 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
       const char* dOs = Qs + TILE;
       const float* Ls = reinterpret_cast<const float*>(Qs + 2 * TILE);
       const float* Ds = Ls + BQ;
-      f32x16 s[2], dp[2];
+      f32x16 s[NT], dp[NT];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < NT; ++t) {
         s[t] = zero16();
         dp[t] = zero16();
         if constexpr (F32) {
@@ -375,7 +382,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
       // P = exp2(S*c - L2[q]); dS = P (dP - delta[q]); rows (q) are in registers
       const bool need_mask = CAUSAL && (qt0 < kw0 + 31);
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int qr = 32 * t + 8 * g + 4 * hh;
@@ -396,7 +403,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
+          for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int qr = 32 * t + acc_row(r, hh);
@@ -404,9 +411,9 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
               dk[dt] = mma_f32(lds_f1<RB>(Qs, qr, dt * 32 + l32), dp[t][r], dk[dt]);
             }
       } else {
-        typename Mma16<T>::frag pf[2][2], sf[2][2];
+        typename Mma16<T>::frag pf[NT][2], sf[NT][2];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < NT; ++t) {
           pf[t][0] = pack_acc<T>(s[t], 0);
           pf[t][1] = pack_acc<T>(s[t], 1);
           sf[t][0] = pack_acc<T>(dp[t], 0);
@@ -415,7 +422,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
+          for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
               dv[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(dOs, 32 * t, s2, dt, lane), pf[t][s2], dv[dt]);

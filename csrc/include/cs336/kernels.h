@@ -20,13 +20,20 @@ int rmsnorm_bwd_workspace_rows(int64_t M, int64_t H);
 // ---- RoPE (csrc/ops/rope.hip) ----
 // x: (B,H,N,D) strided (elements), out: contiguous (B,N,H,D); cos/sin: (ctx, D/2) fp32;
 // pos: (B,N) int64 or nullptr (position = n).
-void rope(const void* x, DType t, int64_t sb, int64_t sh, int64_t sn, void* out, const float* cos_, const float* sin_,
-          const int64_t* pos, int B, int H, int N, int D, bool inverse, hipStream_t s);
+struct RopeArgs {
+  const void* x;
+  int64_t x_sb, x_sh, x_sn;
+  void* out;
+  int64_t o_sb, o_sh, o_sn;
+};
+void rope(const RopeArgs& a, DType t, const float* cos_, const float* sin_, const int64_t* pos, int B, int H, int N,
+          int D, bool inverse, hipStream_t s);
 
 // ---- SwiGLU gate (csrc/ops/swiglu.hip) ----
-void silu_mul_fwd(const void* a, const void* b, void* h, DType t, int64_t n, hipStream_t s);
-void silu_mul_bwd(const void* dh, const void* a, const void* b, void* da, void* db, DType t, int64_t n,
-                  hipStream_t s);
+// (M, F) elementwise; a/b/da/db rows at stride ld (elements), h/dh contiguous. M == 1 allows any F.
+void silu_mul_fwd(const void* a, const void* b, void* h, DType t, int64_t M, int64_t F, int64_t ld, hipStream_t s);
+void silu_mul_bwd(const void* dh, const void* a, const void* b, void* da, void* db, DType t, int64_t M, int64_t F,
+                  int64_t ld, hipStream_t s);
 
 // ---- cross entropy (csrc/ops/xent.hip) ----
 void xent_fwd(const void* z, DType t, const int64_t* tgt, float* loss, float* lse, int64_t M, int64_t V,
@@ -46,8 +53,11 @@ struct TensorTable {
 constexpr int64_t kMTChunk = 32768;  // elements per workgroup chunk
 
 // scalars are rounded to fp32 from double exactly like the reference's Python-float * fp32-tensor ops
-void adamw_step(const TensorTable& tt, DType grad_t, float beta1, float beta2, float one_minus_beta1,
+// table pointers per tensor: p, g, m, v (+ bf16 shadow when shadow == true)
+void adamw_step(const TensorTable& tt, DType grad_t, bool shadow, float beta1, float beta2, float one_minus_beta1,
                 float one_minus_beta2, float eps, float lr_wd, float alpha_t, hipStream_t s);
+// table pointers per tensor: fp32 src, bf16 dst
+void multi_tensor_cast_bf16(const TensorTable& tt, hipStream_t s);
 void multi_tensor_sumsq(const TensorTable& tt, DType t, float* partials, hipStream_t s);
 void finalize_l2norm(const float* partials, int64_t n, float* out, hipStream_t s);
 void multi_tensor_scale(const TensorTable& tt, DType t, const float* scale, hipStream_t s);

@@ -1,30 +1,17 @@
 // SwiGLU gate h = silu(a) * b and its backward, for MI355X.
 //
 // Semantics: reference cs336-basics/cs336_basics/model.py:396-397, 526-527 (silu(x)=x*sigmoid(x)).
-// Memory-bound: every lane moves 16 B per access (8 bf16 or 4 fp32; Guideline 13), grid-stride
-// over the flattened tensor. Backward fuses da = dh*b*s*(1+a*(1-s)) and db = dh*a*s into one
-// pass over (dh, a, b), writing both gradients.
+// Memory-bound: every lane moves 4 elements per access (16 B fp32 / 8 B bf16; Guideline 13),
+// grid-stride over (M rows x F columns). a and b may be row-strided views: the fused W1|W3
+// projection produces one (M, 2F) tensor whose column halves are a and b, so the gate reads it in
+// place, and the backward writes da | db straight into the two halves of one (M, 2F) gradient —
+// the fused GEMM's dY — with no split/cat copies. The backward is a single pass over (dh, a, b).
 #include "cs336/kernels.h"
 
 namespace cs336 {
 namespace {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
-
-template <typename T>
-__global__ __launch_bounds__(256) void silu_mul_fwd_kernel(const typename Elem<T>::storage* __restrict__ a,
-                                                           const typename Elem<T>::storage* __restrict__ b,
-                                                           typename Elem<T>::storage* __restrict__ h, int64_t n4) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    const float4 av = load4<T>(a + 4 * i), bv = load4<T>(b + 4 * i);
-    float4 o;
-    o.x = av.x * sigmoidf_(av.x) * bv.x;
-    o.y = av.y * sigmoidf_(av.y) * bv.y;
-    o.z = av.z * sigmoidf_(av.z) * bv.z;
-    o.w = av.w * sigmoidf_(av.w) * bv.w;
-    store4<T>(h + 4 * i, o);
-  }
-}
 
 __device__ __forceinline__ void silu_mul_grad(float dh, float a, float b, float& da, float& db) {
   const float s = sigmoidf_(a);
@@ -33,25 +20,47 @@ __device__ __forceinline__ void silu_mul_grad(float dh, float a, float b, float&
   da = dh * b * (s + sa * (1.f - s));
 }
 
+// element (r, c) of a/b/da/db at r*ld + c; h/dh contiguous (M, F)
+template <typename T>
+__global__ __launch_bounds__(256) void silu_mul_fwd_kernel(const typename Elem<T>::storage* __restrict__ a,
+                                                           const typename Elem<T>::storage* __restrict__ b,
+                                                           typename Elem<T>::storage* __restrict__ h, int64_t M,
+                                                           int64_t F, int64_t ld) {
+  const int64_t F4 = F >> 2, n4 = M * F4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / F4, c = 4 * (i - r * F4);
+    const float4 av = load4<T>(a + r * ld + c), bv = load4<T>(b + r * ld + c);
+    float4 o;
+    o.x = av.x * sigmoidf_(av.x) * bv.x;
+    o.y = av.y * sigmoidf_(av.y) * bv.y;
+    o.z = av.z * sigmoidf_(av.z) * bv.z;
+    o.w = av.w * sigmoidf_(av.w) * bv.w;
+    store4<T>(h + r * F + c, o);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void silu_mul_bwd_kernel(const typename Elem<T>::storage* __restrict__ dh,
                                                            const typename Elem<T>::storage* __restrict__ a,
                                                            const typename Elem<T>::storage* __restrict__ b,
                                                            typename Elem<T>::storage* __restrict__ da,
-                                                           typename Elem<T>::storage* __restrict__ db, int64_t n4) {
+                                                           typename Elem<T>::storage* __restrict__ db, int64_t M,
+                                                           int64_t F, int64_t ld) {
+  const int64_t F4 = F >> 2, n4 = M * F4;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    const float4 g = load4<T>(dh + 4 * i), av = load4<T>(a + 4 * i), bv = load4<T>(b + 4 * i);
+    const int64_t r = i / F4, c = 4 * (i - r * F4);
+    const float4 g = load4<T>(dh + r * F + c), av = load4<T>(a + r * ld + c), bv = load4<T>(b + r * ld + c);
     float4 oa, ob;
     silu_mul_grad(g.x, av.x, bv.x, oa.x, ob.x);
     silu_mul_grad(g.y, av.y, bv.y, oa.y, ob.y);
     silu_mul_grad(g.z, av.z, bv.z, oa.z, ob.z);
     silu_mul_grad(g.w, av.w, bv.w, oa.w, ob.w);
-    store4<T>(da + 4 * i, oa);
-    store4<T>(db + 4 * i, ob);
+    store4<T>(da + r * ld + c, oa);
+    store4<T>(db + r * ld + c, ob);
   }
 }
 
-// tail (n % 4 elements) handled by a scalar kernel
+// scalar tail for flat (M = 1) calls whose length is not a multiple of 4
 template <typename T>
 __global__ void silu_mul_tail(const typename Elem<T>::storage* a, const typename Elem<T>::storage* b,
                               typename Elem<T>::storage* h, int64_t start, int64_t n) {
@@ -75,36 +84,40 @@ __global__ void silu_mul_bwd_tail(const typename Elem<T>::storage* dh, const typ
 }
 
 template <typename T>
-void fwd_impl(const void* a, const void* b, void* h, int64_t n, hipStream_t s) {
+void fwd_impl(const void* a, const void* b, void* h, int64_t M, int64_t F, int64_t ld, hipStream_t s) {
   typedef typename Elem<T>::storage S;
-  const int64_t n4 = n / 4;
-  if (n4) hipLaunchKernelGGL(silu_mul_fwd_kernel<T>, dim3(stream_grid(n4, 256)), dim3(256), 0, s, (const S*)a, (const S*)b, (S*)h, n4);
-  if (n % 4) hipLaunchKernelGGL(silu_mul_tail<T>, dim3(1), dim3(64), 0, s, (const S*)a, (const S*)b, (S*)h, n4 * 4, n);
+  const int64_t Fv = F & ~(int64_t)3;  // tail only possible when M == 1
+  if (Fv)
+    hipLaunchKernelGGL(silu_mul_fwd_kernel<T>, dim3(stream_grid(M * (Fv / 4), 256)), dim3(256), 0, s, (const S*)a,
+                       (const S*)b, (S*)h, M, Fv, M == 1 ? Fv : ld);
+  if (F != Fv) hipLaunchKernelGGL(silu_mul_tail<T>, dim3(1), dim3(64), 0, s, (const S*)a, (const S*)b, (S*)h, Fv, F);
 }
 template <typename T>
-void bwd_impl(const void* dh, const void* a, const void* b, void* da, void* db, int64_t n, hipStream_t s) {
+void bwd_impl(const void* dh, const void* a, const void* b, void* da, void* db, int64_t M, int64_t F, int64_t ld,
+              hipStream_t s) {
   typedef typename Elem<T>::storage S;
-  const int64_t n4 = n / 4;
-  if (n4)
-    hipLaunchKernelGGL(silu_mul_bwd_kernel<T>, dim3(stream_grid(n4, 256)), dim3(256), 0, s, (const S*)dh, (const S*)a,
-                       (const S*)b, (S*)da, (S*)db, n4);
-  if (n % 4)
+  const int64_t Fv = F & ~(int64_t)3;
+  if (Fv)
+    hipLaunchKernelGGL(silu_mul_bwd_kernel<T>, dim3(stream_grid(M * (Fv / 4), 256)), dim3(256), 0, s, (const S*)dh,
+                       (const S*)a, (const S*)b, (S*)da, (S*)db, M, Fv, M == 1 ? Fv : ld);
+  if (F != Fv)
     hipLaunchKernelGGL(silu_mul_bwd_tail<T>, dim3(1), dim3(64), 0, s, (const S*)dh, (const S*)a, (const S*)b, (S*)da,
-                       (S*)db, n4 * 4, n);
+                       (S*)db, Fv, F);
 }
 
 }  // namespace
 
-void silu_mul_fwd(const void* a, const void* b, void* h, DType t, int64_t n, hipStream_t s) {
-  if (t == DType::F32) fwd_impl<float>(a, b, h, n, s);
-  else if (t == DType::BF16) fwd_impl<BF16>(a, b, h, n, s);
-  else fwd_impl<F16>(a, b, h, n, s);
+void silu_mul_fwd(const void* a, const void* b, void* h, DType t, int64_t M, int64_t F, int64_t ld, hipStream_t s) {
+  if (t == DType::F32) fwd_impl<float>(a, b, h, M, F, ld, s);
+  else if (t == DType::BF16) fwd_impl<BF16>(a, b, h, M, F, ld, s);
+  else fwd_impl<F16>(a, b, h, M, F, ld, s);
 }
 
-void silu_mul_bwd(const void* dh, const void* a, const void* b, void* da, void* db, DType t, int64_t n, hipStream_t s) {
-  if (t == DType::F32) bwd_impl<float>(dh, a, b, da, db, n, s);
-  else if (t == DType::BF16) bwd_impl<BF16>(dh, a, b, da, db, n, s);
-  else bwd_impl<F16>(dh, a, b, da, db, n, s);
+void silu_mul_bwd(const void* dh, const void* a, const void* b, void* da, void* db, DType t, int64_t M, int64_t F,
+                  int64_t ld, hipStream_t s) {
+  if (t == DType::F32) bwd_impl<float>(dh, a, b, da, db, M, F, ld, s);
+  else if (t == DType::BF16) bwd_impl<BF16>(dh, a, b, da, db, M, F, ld, s);
+  else bwd_impl<F16>(dh, a, b, da, db, M, F, ld, s);
 }
 
 }  // namespace cs336

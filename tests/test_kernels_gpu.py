@@ -238,3 +238,74 @@ def test_model_bf16_autocast_step():
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < losses[0]
+
+
+# ---------------------------------------------------------------------------------- fused layout
+def test_swiglu_fused_matches_reference():
+    from cs336_systems.models.fused import SwiGLUGate
+
+    torch.manual_seed(0)
+    F = 384
+    y = torch.randn(5, 7, 2 * F, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    h = SwiGLUGate.apply(y)
+    yr = y.detach().float().requires_grad_(True)
+    hr = ops.silu_mul_ref(yr[..., :F], yr[..., F:])
+    torch.testing.assert_close(h.float(), hr, rtol=2e-2, atol=2e-2)
+    g = torch.randn_like(hr)
+    h.backward(g.bfloat16())
+    hr.backward(g.bfloat16().float())
+    torch.testing.assert_close(y.grad.float(), yr.grad, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_fused_layout_matches_unfused(amp):
+    """Grouped QKV / W1|W3 GEMMs + AttentionCore + fp32-out dW == the unfused GPU path."""
+    from cs336_systems.models import BasicsTransformerLM
+
+    torch.manual_seed(0)
+    cfg = dict(vocab_size=500, context_length=128, d_model=256, num_layers=2, num_heads=4, d_ff=512, rope_theta=10000.0)
+    m_f = BasicsTransformerLM(**cfg, device=DEV, fused_layout=True)
+    m_u = BasicsTransformerLM(**cfg, device=DEV, fused_layout=False)
+    m_u.load_state_dict(m_f.state_dict())
+    from cs336_systems.models.fused import grouped_view
+
+    assert grouped_view([m_f.layers[0].attn.q_proj.weight, m_f.layers[0].attn.k_proj.weight, m_f.layers[0].attn.v_proj.weight]) is not None
+    assert grouped_view([m_u.layers[0].attn.q_proj.weight, m_u.layers[0].attn.k_proj.weight, m_u.layers[0].attn.v_proj.weight]) is None
+    x = torch.randint(0, 500, (2, 128), device=DEV)
+    outs = []
+    for m in (m_f, m_u):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            loss = ops.cross_entropy(m(x), x)
+        loss.backward()
+        outs.append((loss.detach(), {n: p.grad for n, p in m.named_parameters()}))
+    tol = 2e-2 if amp else 1e-3
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=tol, atol=tol)
+    for n, g in outs[0][1].items():
+        assert g.dtype == torch.float32
+        torch.testing.assert_close(g, outs[1][1][n], rtol=5e-2 if amp else 2e-3, atol=5e-3 if amp else 1e-4, msg=n)
+
+
+def test_bf16_shadows_track_master_weights():
+    from cs336_systems.models import build_model
+    from cs336_systems.models.fused import get_shadow, shadow_valid
+
+    torch.manual_seed(0)
+    m = build_model("tiny", 64, device=DEV)
+    opt = ops.FusedAdamW(m.parameters(), lr=1e-2, bf16_shadows=True)
+    w = m.layers[0].attn.q_proj.weight
+    assert shadow_valid(w)
+    assert torch.equal(get_shadow(w), w.detach().bfloat16())
+    x = torch.randint(0, 10000, (2, 64), device=DEV)
+    for _ in range(2):
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = ops.cross_entropy(m(x), x)
+        loss.backward()
+        opt.step()
+        for p in m.parameters():
+            if p.dim() == 2:
+                assert shadow_valid(p)
+                assert torch.equal(get_shadow(p), p.detach().bfloat16())
+    with torch.no_grad():
+        w.add_(1.0)  # out-of-band edit invalidates the shadow -> forward falls back to casting
+    assert not shadow_valid(w)
