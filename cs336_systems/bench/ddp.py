@@ -1,0 +1,198 @@
+"""Data-parallel training driver (reference ``naive_ddp.py`` train/train_ddp/train_ddp_flat and
+``ddp_bucketed_overlapped_sharded.py`` train_process/train_process_ddp; handout §2.2-2.3).
+
+Trains the Transformer LM with one of the DP variants and reports per-step time split into
+forward / backward / gradient-communication wait / optimizer, the communication fraction, loss,
+and peak memory after init / before the optimizer step / after it (the sharded-optimizer
+accounting of handout §2.3.1). Ranks come from torchrun's env or ``--world-size`` (mp.spawn);
+``--cpu`` runs Gloo on CPU (the reference's tested configuration), otherwise RCCL on GPU.
+
+Correctness mode (``--check``): every rank also trains an unwrapped replica on the full global
+batch and asserts the DP model's parameters match it after every step (what the reference's
+``naive_ddp.main`` meant to do before its NameError).
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m cs336_systems.bench.ddp --variant bucketed --size xl --ctx 512 --batch 128
+    python -m cs336_systems.bench.ddp --cpu --world-size 2 --size tiny --ctx 32 --batch 8 --variant naive --check
+"""
+
+from __future__ import annotations
+
+import argparse
+import copy
+import contextlib
+import json
+import os
+import statistics
+import time
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..data import synthetic_batch
+from ..models import build_model
+from ..parallel import DDP_VARIANTS, DEFAULT_BUCKET_MB, ShardedOptimizer, cleanup_distributed, setup_distributed, spawn, wrap_ddp
+from ..utils.profiling import annotate
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _mem(dev):
+    return torch.cuda.memory_allocated(dev) / 2**20 if dev.type == "cuda" else 0.0
+
+
+def _peak(dev):
+    return torch.cuda.max_memory_allocated(dev) / 2**20 if dev.type == "cuda" else 0.0
+
+
+def train_ddp(rank: int, world: int, args) -> dict | None:
+    backend = "gloo" if args.cpu else None
+    rank, world, dev = setup_distributed(rank, world, backend=backend)
+    torch.manual_seed(args.seed)
+    model = build_model(args.size, args.ctx, device=dev)
+    if args.check:
+        ref = copy.deepcopy(model)
+        for p in ref.parameters():
+            dist.broadcast(p.data, 0)
+        # Adam normalizes each update to ~lr, so summation-order differences in near-zero gradient
+        # entries can move a parameter by up to ~2*lr per step: scale the tolerance accordingly
+        check_tol = args.check_tol if args.check_tol is not None else 2.0 * args.lr * (args.steps + args.warmup) + 1e-6
+    ddp = wrap_ddp(model, args.variant, bucket_size_mb=args.bucket_mb)
+    okw = dict(lr=args.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=args.wd)
+    if args.sharded:
+        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, **okw)
+    else:
+        opt = ops.FusedAdamW(model.parameters(), **okw)
+    ref_opt = ops.FusedAdamW(ref.parameters(), **okw) if args.check else None
+    mem_init = _mem(dev)
+    assert args.batch % world == 0, "global batch must divide by world size"
+    local = args.batch // world
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed)  # same global batches on every rank; each rank slices its part
+    amp = (not args.cpu) and args.dtype == "bf16"
+    autocast = (lambda: torch.autocast(dev.type, dtype=torch.bfloat16)) if amp else contextlib.nullcontext
+    rec = {k: [] for k in ("fwd", "bwd", "comm", "opt", "step")}
+    losses, mem_before, mem_after = [], [], []
+    for it in range(args.warmup + args.steps):
+        x, y = synthetic_batch(args.batch, args.ctx, 10000, dev, gen)
+        xs, ys = x[rank * local : (rank + 1) * local], y[rank * local : (rank + 1) * local]
+        timed = it >= args.warmup
+        _sync(dev)
+        t0 = time.perf_counter()
+        if hasattr(ddp, "zero_grad") and args.variant in ("bucketed", "flat"):
+            ddp.zero_grad()
+        else:
+            opt.zero_grad(set_to_none=True)
+        with autocast():
+            loss = ops.cross_entropy(ddp(xs), ys)
+        _sync(dev)
+        t1 = time.perf_counter()
+        with annotate("backward"):
+            loss.backward()
+        _sync(dev)
+        t2 = time.perf_counter()
+        with annotate("grad_sync"):
+            ddp.finish_gradient_synchronization()
+        _sync(dev)
+        t3 = time.perf_counter()
+        if args.clip > 0:
+            ops.clip_grad_norm_(model.parameters(), args.clip)
+        mem_before.append(_peak(dev))
+        opt.step()
+        _sync(dev)
+        t4 = time.perf_counter()
+        mem_after.append(_peak(dev))
+        if timed:
+            for k, v in zip(("fwd", "bwd", "comm", "opt", "step"), (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t4 - t0)):
+                rec[k].append(v * 1e3)
+        lt = loss.detach().clone()
+        if dist.get_backend() == "nccl":
+            dist.all_reduce(lt, op=dist.ReduceOp.AVG)
+        else:
+            dist.all_reduce(lt)
+            lt /= world
+        losses.append(float(lt))
+        if args.check:
+            ref_opt.zero_grad(set_to_none=True)
+            with autocast():
+                ops.cross_entropy(ref(x), y).backward()
+            if args.clip > 0:
+                ops.clip_grad_norm_(ref.parameters(), args.clip)
+            ref_opt.step()
+            worst = max((a - b).abs().max().item() for a, b in zip(model.parameters(), ref.parameters()))
+            assert worst < check_tol, f"rank {rank} step {it}: DP params diverge from single-process ({worst:.3e})"
+    out = None
+    stats = {k: (statistics.fmean(v) if v else 0.0) for k, v in rec.items()}
+    t = torch.tensor([stats[k] for k in ("fwd", "bwd", "comm", "opt", "step")], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        fwd, bwd, comm, optt, step = (float(v) for v in t.tolist())
+        out = dict(
+            variant=args.variant,
+            sharded=args.sharded,
+            world=world,
+            size=args.size,
+            ctx=args.ctx,
+            global_batch=args.batch,
+            bucket_mb=args.bucket_mb if args.variant == "bucketed" else None,
+            fwd_ms=fwd,
+            bwd_ms=bwd,
+            comm_wait_ms=comm,
+            opt_ms=optt,
+            step_ms=step,
+            comm_fraction=comm / step if step else 0.0,
+            tokens_per_s=args.batch * args.ctx / (step / 1e3) if step else 0.0,
+            final_loss=losses[-1],
+            mem_after_init_mib=mem_init,
+            peak_before_step_mib=max(mem_before) if mem_before else 0.0,
+            peak_after_step_mib=max(mem_after) if mem_after else 0.0,
+            checked=bool(args.check),
+        )
+        print(json.dumps(out), flush=True)
+        if args.json:
+            with open(args.json, "w") as f:
+                json.dump(out, f, indent=1)
+    cleanup_distributed()
+    return out
+
+
+def _spawned(rank, world, args):
+    train_ddp(rank, world, args)
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--variant", default="bucketed", choices=sorted(DDP_VARIANTS))
+    ap.add_argument("--bucket-mb", type=float, default=DEFAULT_BUCKET_MB)
+    ap.add_argument("--sharded", action="store_true")
+    ap.add_argument("--size", default="xl")
+    ap.add_argument("--ctx", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=16, help="global batch (split over ranks)")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--wd", type=float, default=0.01)
+    ap.add_argument("--clip", type=float, default=0.0)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--world-size", type=int, default=2)
+    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--check-tol", type=float, default=None)
+    ap.add_argument("--json", default=None)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
+        train_ddp(int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]), args)
+    else:
+        spawn(_spawned, args.world_size, args)
+
+
+if __name__ == "__main__":
+    main()
