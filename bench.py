@@ -143,10 +143,8 @@ def main(argv=None):
     batches = [synthetic_batch(args.batch, args.ctx, args.vocab, device, gen) for _ in range(4)]
 
     def zero_grads():
-        if hasattr(ddp_model, "zero_grad") and world > 1 and args.ddp in ("bucketed", "flat"):
-            ddp_model.zero_grad()
-        else:
-            opt.zero_grad(set_to_none=True)
+        # unset grads: the projection GEMMs then write fp32 dW straight into the DDP buckets
+        opt.zero_grad(set_to_none=True)
 
     def step(i):
         x, y = batches[i % len(batches)]

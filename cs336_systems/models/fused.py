@@ -174,7 +174,18 @@ class FusedLinearFn(torch.autograd.Function):
         ctx.x_dtype = x.dtype
         ctx.rows = [p.shape[0] for p in weights]
         ctx.wdtype = [p.dtype for p in weights]
+        ctx.weights = weights
         return y.view(*x.shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def _grad_target(weights) -> torch.Tensor | None:
+        """A DDP bucket region to write dW into (all grads unset, fp32, row-adjacent views)."""
+        outs = [getattr(p, "_cs336_grad_out", None) for p in weights]
+        if any(o is None for o in outs) or any(p.grad is not None for p in weights):
+            return None
+        if outs[0].dtype != torch.float32:
+            return None
+        return _adjacent_rows(outs)
 
     @staticmethod
     def backward(ctx, dy):
@@ -188,7 +199,12 @@ class FusedLinearFn(torch.autograd.Function):
             if dx.dtype != ctx.x_dtype:
                 dx = dx.to(ctx.x_dtype)
         if any(ctx.needs_input_grad[1:]):
-            dw = _mm_fp32_out(dy2.t(), x2)
+            target = FusedLinearFn._grad_target(ctx.weights) if dy2.dtype == torch.bfloat16 else None
+            if target is not None:
+                torch.mm(dy2.t(), x2, out_dtype=torch.float32, out=target)
+                dw = target
+            else:
+                dw = _mm_fp32_out(dy2.t(), x2)
             dw_parts = list(torch.split(dw, ctx.rows, 0))
             dw_parts = [g if g.dtype == dt else g.to(dt) for g, dt in zip(dw_parts, ctx.wdtype)]
         return (dx, *(dw_parts if dw_parts is not None else [None] * len(ctx.rows)))
@@ -202,43 +218,49 @@ def fused_linear(x: torch.Tensor, *weights: nn.Parameter) -> torch.Tensor:
 # attention core on the fused QKV layout
 # ------------------------------------------------------------------------------------------
 class AttentionCore(torch.autograd.Function):
-    """qkv (B, N, 3*H*dk) -> RoPE(q), RoPE(k) -> causal FA2 -> o as a (B, H, N, dk) view of
-    (B, N, H, dk) memory. Backward returns d(qkv) in the same fused layout: FA2 writes dq, dk, dv
-    straight into the three slices of one buffer, then the inverse rotation runs in place."""
+    """qkv (B, N, 3*H*dk) -> RoPE(q|k) -> causal FA2 -> o as a (B, H, N, dk) view of
+    (B, N, H, dk) memory.
+
+    Q and K heads are adjacent in the fused projection output, so one RoPE launch rotates both as
+    a (B, 2H, N, dk) view. The backward writes dq, dk, dv straight into the three slices of one
+    fused d(qkv) buffer, then one in-place inverse rotation covers dq|dk. No split/cat copies.
+
+    (The FA kernels can also rotate Q/K on load — ``fa_fwd(..., cos, sin, pos)`` — but at
+    N=512 that re-rotates every K tile once per query block and measured ~5 % slower per XL step
+    than this one O(N) pass; see profiles/README.md.)"""
+
+    @staticmethod
+    def _split(t, H):
+        B, N, three_d = t.shape
+        dk = three_d // (3 * H)
+        t5 = t.view(B, N, 3, H, dk)
+        qk = t5[:, :, 0:2].reshape(B, N, 2 * H, dk).transpose(1, 2)  # view: (B, 2H, N, dk)
+        return qk, t5[:, :, 2].transpose(1, 2)
 
     @staticmethod
     def forward(ctx, qkv, cos, sin, pos, H):
-        B, N, three_d = qkv.shape
-        dk = three_d // (3 * H)
-        y5 = qkv.view(B, N, 3, H, dk)
-        q_in = y5[:, :, 0].transpose(1, 2)
-        k_in = y5[:, :, 1].transpose(1, 2)
-        v = y5[:, :, 2].transpose(1, 2)
+        qk_in, v = AttentionCore._split(qkv, H)
         hip = _hip()
-        q = hip.rope(q_in, cos, sin, pos, False)
-        k = hip.rope(k_in, cos, sin, pos, False)
-        scale = dk**-0.5
+        qk = hip.rope(qk_in, cos, sin, pos, False)
+        q, k = qk[:, :H], qk[:, H:]
+        scale = q.shape[-1] ** -0.5
         o, lse = hip.fa_fwd(q, k, v, True, scale)
-        ctx.save_for_backward(q, k, qkv, o, lse, cos, sin, pos)
+        ctx.save_for_backward(qk, v, o, lse, cos, sin, pos)
         ctx.H, ctx.scale = H, scale
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, qkv, o, lse, cos, sin, pos = ctx.saved_tensors
-        B, N, three_d = qkv.shape
+        qk, v, o, lse, cos, sin, pos = ctx.saved_tensors
         H = ctx.H
-        dk = three_d // (3 * H)
-        v = qkv.view(B, N, 3, H, dk)[:, :, 2].transpose(1, 2)
-        dqkv = torch.empty_like(qkv)
-        d5 = dqkv.view(B, N, 3, H, dk)
-        dq, dkk, dv = (d5[:, :, i].transpose(1, 2) for i in range(3))
+        B, N = v.shape[0], v.shape[2]
+        dqkv = torch.empty(B, N, 3 * H * v.shape[3], dtype=v.dtype, device=v.device)
+        dqk, dv = AttentionCore._split(dqkv, H)
         if do.stride(-1) != 1:
             do = do.contiguous()
         hip = _hip()
-        hip.fa_bwd_into(do, q, k, v, o, lse, True, ctx.scale, dq, dkk, dv)
-        hip.rope_into(dq, cos, sin, pos, True, dq)
-        hip.rope_into(dkk, cos, sin, pos, True, dkk)
+        hip.fa_bwd_into(do, qk[:, :H], qk[:, H:], v, o, lse, True, ctx.scale, dqk[:, :H], dqk[:, H:], dv)
+        hip.rope_into(dqk, cos, sin, pos, True, dqk)
         return dqkv, None, None, None, None
 
 

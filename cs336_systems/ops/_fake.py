@@ -13,13 +13,13 @@ def _bnhd_like(q):
 
 
 @register_fake("cs336::fa_fwd")
-def _fa_fwd(q, k, v, causal, scale):
+def _fa_fwd(q, k, v, causal, scale, rope_cos=None, rope_sin=None, rope_pos=None):
     B, H, N, D = q.shape
     return _bnhd_like(q), q.new_empty((B, H, N), dtype=torch.float32)
 
 
 @register_fake("cs336::fa_bwd")
-def _fa_bwd(do, q, k, v, o, lse, causal, scale):
+def _fa_bwd(do, q, k, v, o, lse, causal, scale, rope_cos=None, rope_sin=None, rope_pos=None):
     return _bnhd_like(q), _bnhd_like(k), _bnhd_like(v)
 
 
@@ -65,7 +65,7 @@ def _l2(ts):
 
 
 @register_fake("cs336::fa_bwd_into")
-def _fa_bwd_into(do, q, k, v, o, lse, causal, scale, dq, dk, dv):
+def _fa_bwd_into(do, q, k, v, o, lse, causal, scale, dq, dk, dv, rope_cos=None, rope_sin=None, rope_pos=None):
     return None
 
 

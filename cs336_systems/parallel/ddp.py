@@ -102,6 +102,7 @@ class FlatDDP(_DDPBase):
             off = 0
             for p in ps:
                 self._views[p] = flat[off : off + p.numel()].view_as(p)
+                p._cs336_grad_out = self._views[p]  # GEMMs may write dW here directly
                 off += p.numel()
             self._groups[key] = (flat, ps)
         self.zero_grad()
@@ -167,9 +168,9 @@ class DDPBucketed(_DDPBase):
     backward produces gradients) up to ``bucket_size_mb`` (``None`` → one unbounded bucket);
     a bucket never mixes dtypes/devices. Each parameter's ``.grad`` is a view into its bucket's
     flat buffer, so autograd accumulates straight into the communication buffer. If a caller
-    resets grads to ``None`` (``optimizer.zero_grad()``), the hook copies the fresh gradient into
-    the view once and re-attaches it; calling :meth:`zero_grad` (or
-    ``on_train_batch_start``) instead keeps the zero-copy path.
+    resets grads to ``None`` (``optimizer.zero_grad()``), the projection GEMMs of the model write
+    their fp32 dW directly into the bucket (``p._cs336_grad_out``; no memset, no accumulate add,
+    no copy) and any other fresh gradient is copied into its view once by the hook.
     """
 
     def __init__(self, module: nn.Module, bucket_size_mb: float | None = DEFAULT_BUCKET_MB, process_group=None, broadcast: bool = True):
@@ -177,15 +178,29 @@ class DDPBucketed(_DDPBase):
         self.bucket_size_mb = bucket_size_mb
         cap = float("inf") if bucket_size_mb is None else bucket_size_mb * 1024 * 1024
         params = [p for p in _unique_params(module) if p.requires_grad]
+        # parameters that share one storage (the fused QKV / W1|W3 layout of models/fused.py) form
+        # an indivisible unit laid out in storage order, so the grouped dW GEMM can write all of
+        # them into one contiguous region of the bucket
+        by_storage: dict[int, list[nn.Parameter]] = {}
+        for p in params:
+            by_storage.setdefault(p.untyped_storage().data_ptr(), []).append(p)
+        units, seen = [], set()
+        for p in reversed(params):
+            key = p.untyped_storage().data_ptr()
+            if key in seen:
+                continue
+            seen.add(key)
+            units.append(sorted(by_storage[key], key=lambda t: t.storage_offset()))
         groups: list[list[nn.Parameter]] = []
         cur: list[nn.Parameter] = []
         cur_bytes = 0
-        for p in reversed(params):
-            nbytes = p.numel() * p.element_size()
+        for unit in units:
+            nbytes = sum(p.numel() * p.element_size() for p in unit)
+            p = unit[0]
             if cur and (cur_bytes + nbytes > cap or p.dtype != cur[0].dtype or p.device != cur[0].device):
                 groups.append(cur)
                 cur, cur_bytes = [], 0
-            cur.append(p)
+            cur.extend(unit)
             cur_bytes += nbytes
         if cur:
             groups.append(cur)
@@ -203,6 +218,9 @@ class DDPBucketed(_DDPBase):
             self.buckets.append(b)
             for p in ps:
                 self._param_bucket[p] = b
+                # GEMM-output target: FusedLinearFn writes dW straight into the bucket when the
+                # grad is unset (models/fused.py), so _adopt finds it already in place
+                p._cs336_grad_out = self._views[p]
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in params]
         self.zero_grad()
 

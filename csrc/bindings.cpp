@@ -73,8 +73,31 @@ void fill_attn(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, c
   p.causal = causal;
 }
 
+using OptT = std::optional<at::Tensor>;
+
+// fused RoPE: q/k are the un-rotated projections; cos/sin (ctx, D/2) fp32, pos (B, N) int64 or None
+void set_rope(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, const OptT& cos, const OptT& sin,
+              const OptT& pos) {
+  if (!cos.has_value() || !cos->defined()) return;
+  TORCH_CHECK(sin.has_value() && sin->defined(), "cs336: rope needs cos and sin");
+  TORCH_CHECK(cos->scalar_type() == at::kFloat && cos->is_contiguous() && sin->is_contiguous() &&
+                  cos->size(1) * 2 == q.size(3),
+              "cs336: rope cache must be contiguous fp32 (ctx, D/2)");
+  TORCH_CHECK(q.size(2) == k.size(2), "cs336: fused rope is for self-attention (Nq == Nk)");
+  if (pos.has_value() && pos->defined()) {
+    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->is_contiguous() && pos->numel() == q.size(0) * q.size(2),
+                "cs336: rope positions must be contiguous int64 (B, N)");
+    p.rope_pos = pos->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(q.size(2) <= cos->size(0), "cs336: sequence longer than the RoPE cache");
+  }
+  p.rope_cos = cos->data_ptr<float>();
+  p.rope_sin = sin->data_ptr<float>();
+}
+
 std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bool causal,
-                                          double scale) {
+                                          double scale, const OptT& rope_cos, const OptT& rope_sin,
+                                          const OptT& rope_pos) {
   check_bhnd(q, "q");
   check_bhnd(k, "k");
   check_bhnd(v, "v");
@@ -86,17 +109,18 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
   at::Tensor lse = at::empty({q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
   cs336::AttnParams p;
   fill_attn(p, q, k, v, o, lse, causal, scale);
+  set_rope(p, q, k, rope_cos, rope_sin, rope_pos);
   cs336::flash_attn_fwd(p, to_dtype(q), stream());
   return {o, lse};
 }
 
 void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                 const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
-                const at::Tensor& dk, const at::Tensor& dv);
+                const at::Tensor& dk, const at::Tensor& dv, const OptT& rope_cos, const OptT& rope_sin,
+                const OptT& rope_pos);
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
-                                                      const at::Tensor& v, const at::Tensor& out,
-                                                      const at::Tensor& lse, bool causal, double scale) {
+void check_bwd_inputs(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                      const at::Tensor& out, const at::Tensor& lse) {
   check_bhnd(q, "q");
   check_bhnd(k, "k");
   check_bhnd(v, "v");
@@ -104,11 +128,19 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_bwd(const at::Tensor& dout, co
   check_bhnd(dout, "dout");
   TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == at::kFloat, "cs336: lse must be contiguous fp32");
   TORCH_CHECK(dout.scalar_type() == q.scalar_type() && out.scalar_type() == q.scalar_type(), "cs336: dtype mismatch");
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
+                                                      const at::Tensor& v, const at::Tensor& out,
+                                                      const at::Tensor& lse, bool causal, double scale,
+                                                      const OptT& rope_cos, const OptT& rope_sin,
+                                                      const OptT& rope_pos) {
+  check_bwd_inputs(dout, q, k, v, out, lse);
   c10::DeviceGuard g(q.device());
   at::Tensor dq = empty_bnhd_like(q);
   at::Tensor dk = empty_bnhd_like(k);
   at::Tensor dv = empty_bnhd_like(v);
-  fa_bwd_run(dout, q, k, v, out, lse, causal, scale, dq, dk, dv);
+  fa_bwd_run(dout, q, k, v, out, lse, causal, scale, dq, dk, dv, rope_cos, rope_sin, rope_pos);
   return {dq, dk, dv};
 }
 
@@ -116,30 +148,28 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_bwd(const at::Tensor& dout, co
 // one fused dQKV buffer that feeds the fused QKV-projection GEMM)
 void fa_bwd_into(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                  const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
-                 const at::Tensor& dk, const at::Tensor& dv) {
-  check_bhnd(q, "q");
-  check_bhnd(k, "k");
-  check_bhnd(v, "v");
-  check_bhnd(out, "out");
-  check_bhnd(dout, "dout");
+                 const at::Tensor& dk, const at::Tensor& dv, const OptT& rope_cos, const OptT& rope_sin,
+                 const OptT& rope_pos) {
+  check_bwd_inputs(dout, q, k, v, out, lse);
   check_bhnd(dq, "dq");
   check_bhnd(dk, "dk");
   check_bhnd(dv, "dv");
   TORCH_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "cs336: grad shapes");
   TORCH_CHECK(dq.scalar_type() == q.scalar_type() && dk.scalar_type() == q.scalar_type() &&
-                  dv.scalar_type() == q.scalar_type() && dout.scalar_type() == q.scalar_type(),
+                  dv.scalar_type() == q.scalar_type(),
               "cs336: dtype mismatch");
-  TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == at::kFloat, "cs336: lse must be contiguous fp32");
   c10::DeviceGuard g(q.device());
-  fa_bwd_run(dout, q, k, v, out, lse, causal, scale, dq, dk, dv);
+  fa_bwd_run(dout, q, k, v, out, lse, causal, scale, dq, dk, dv, rope_cos, rope_sin, rope_pos);
 }
 
 void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                 const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
-                const at::Tensor& dk, const at::Tensor& dv) {
+                const at::Tensor& dk, const at::Tensor& dv, const OptT& rope_cos, const OptT& rope_sin,
+                const OptT& rope_pos) {
   at::Tensor delta = at::empty({q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
   cs336::AttnBwdParams bp;
   fill_attn(bp.f, q, k, v, out, lse, causal, scale);
+  set_rope(bp.f, q, k, rope_cos, rope_sin, rope_pos);
   bp.dout = dout.data_ptr();
   bp.do_sb = dout.stride(0); bp.do_sh = dout.stride(1); bp.do_sn = dout.stride(2);
   bp.dq = dq.data_ptr();
@@ -402,16 +432,19 @@ void multi_tensor_scale_(std::vector<at::Tensor> tensors, const at::Tensor& scal
 }  // namespace
 
 TORCH_LIBRARY(cs336, m) {
-  m.def("fa_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
   m.def(
-      "fa_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale) -> "
+      "fa_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None, "
+      "Tensor? rope_pos=None) -> (Tensor, Tensor)");
+  m.def(
+      "fa_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale, "
+      "Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None) -> "
       "(Tensor, Tensor, Tensor)");
   m.def("rmsnorm_fwd(Tensor x, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, Tensor? pos, bool inverse) -> Tensor");
   m.def(
       "fa_bwd_into(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale, "
-      "Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
+      "Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None) -> ()");
   m.def("rope_into(Tensor x, Tensor cos, Tensor sin, Tensor? pos, bool inverse, Tensor(a!) out) -> ()");
   m.def("swiglu_fused_fwd(Tensor y) -> Tensor");
   m.def("swiglu_fused_bwd(Tensor dh, Tensor y) -> Tensor");

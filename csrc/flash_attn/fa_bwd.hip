@@ -24,7 +24,7 @@ namespace fa {
 // ============================================================================================
 // dQ (+ delta) kernel
 // ============================================================================================
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, bool ROPE>
 __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
   const AttnParams p = bp.f;  // by value: a reference would spill the kernarg struct to scratch
@@ -64,6 +64,9 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   S* dQp = (S*)bp.dq + b * bp.dq_sb + h * bp.dq_sh;
   const int64_t row_lin = ((int64_t)b * p.H + h) * p.Nq + qrow;
 
+  const Rope rope{p.rope_cos, p.rope_sin, D / 2};
+  const int64_t* rpos = p.rope_pos ? p.rope_pos + (int64_t)b * p.Nq : nullptr;
+  const int64_t qpos = rpos && valid_q ? rpos[qrow] : qrow;
   constexpr int NQF = F32 ? D / 8 : D / 16;
   uint4 qf[NQF], dof[NQF];
   float delta = 0.f;
@@ -72,6 +75,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
     const int e = F32 ? (hh * (D / 2) + 4 * i) : (16 * i + 8 * hh);
     if (valid_q) {
       qf[i] = *reinterpret_cast<const uint4*>(Qp + (int64_t)qrow * p.q_sn + e);
+      if (ROPE) qf[i] = rope_chunk<T>(qf[i], rope, qpos, e, 1.f);
       dof[i] = *reinterpret_cast<const uint4*>(dOp + (int64_t)qrow * bp.do_sn + e);
       // delta partial over this lane's half of d
 #pragma unroll
@@ -92,12 +96,14 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   const int ntiles = (kv_end + BN - 1) / BN;
 
   uint4 kst[LPT], vst[LPT];
+  RopeCoef kst_rc[ROPE ? LPT : 1];  // rotation applied at LDS-write time (keeps the prefetch async)
   auto gload = [&](int j) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i;
       const int r = c / CPR, ch = c % CPR;
       const int key = j * BN + r;
+      if (ROPE) kst_rc[i] = rope_coef<T>(rope, key < p.Nk ? (rpos ? rpos[key] : key) : 0, ch * EPC);
       if (key < p.Nk) {
         kst[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)key * p.k_sn + ch * EPC);
         vst[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)key * p.v_sn + ch * EPC);
@@ -113,7 +119,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i;
       const int off = lds_off<RB>(c / CPR, c % CPR);
-      *reinterpret_cast<uint4*>(Ks + off) = kst[i];
+      *reinterpret_cast<uint4*>(Ks + off) = ROPE ? rope_apply<T>(kst[i], kst_rc[i]) : kst[i];
       *reinterpret_cast<uint4*>(Ks + TILE + off) = vst[i];
     }
   };
@@ -222,8 +228,10 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d = dt * 32 + 8 * g + 4 * hh;
-        store4<T>(row + d, make_float4(dq[dt][4 * g] * sc, dq[dt][4 * g + 1] * sc, dq[dt][4 * g + 2] * sc,
-                                       dq[dt][4 * g + 3] * sc));
+        float v0 = dq[dt][4 * g] * sc, v1 = dq[dt][4 * g + 1] * sc, v2 = dq[dt][4 * g + 2] * sc,
+              v3 = dq[dt][4 * g + 3] * sc;
+        if (ROPE) rope_inv4(v0, v1, v2, v3, rope, qpos, d);  // dQ w.r.t. the un-rotated q
+        store4<T>(row + d, make_float4(v0, v1, v2, v3));
       }
   }
 }
@@ -231,7 +239,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
 // ============================================================================================
 // dK / dV kernel
 // ============================================================================================
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, bool ROPE>
 __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
   const AttnParams p = bp.f;  // by value: a reference would spill the kernarg struct to scratch
@@ -272,6 +280,9 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
   S* dVp = (S*)bp.dv + b * bp.dv_sb + h * bp.dv_sh;
 
   // K, V fragments (B operands), resident
+  const Rope rope{p.rope_cos, p.rope_sin, D / 2};
+  const int64_t* rpos = p.rope_pos ? p.rope_pos + (int64_t)b * p.Nq : nullptr;
+  const int64_t kpos = rpos && valid_k ? rpos[krow] : krow;
   constexpr int NKF = F32 ? D / 8 : D / 16;
   uint4 kf[NKF], vf[NKF];
 #pragma unroll
@@ -279,6 +290,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
     const int e = F32 ? (hh * (D / 2) + 4 * i) : (16 * i + 8 * hh);
     if (valid_k) {
       kf[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)krow * p.k_sn + e);
+      if (ROPE) kf[i] = rope_chunk<T>(kf[i], rope, kpos, e, 1.f);
       vf[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)krow * p.v_sn + e);
     } else {
       kf[i] = vf[i] = make_uint4(0, 0, 0, 0);
@@ -289,6 +301,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
   const int qt_end = (p.Nq + BQ - 1) / BQ;
 
   uint4 qst[LPT], dst[LPT];
+  RopeCoef qst_rc[ROPE ? LPT : 1];  // rotation applied at LDS-write time (keeps the prefetch async)
   float lst = 0.f, dlt = 0.f;
   auto gload = [&](int it) {
     const int qbase = it * BQ;
@@ -297,6 +310,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
       const int c = tid + 256 * i;
       const int r = c / CPR, ch = c % CPR;
       const int q = qbase + r;
+      if (ROPE) qst_rc[i] = rope_coef<T>(rope, q < p.Nq ? (rpos ? rpos[q] : q) : 0, ch * EPC);
       if (q < p.Nq) {
         qst[i] = *reinterpret_cast<const uint4*>(Qp + (int64_t)q * p.q_sn + ch * EPC);
         dst[i] = *reinterpret_cast<const uint4*>(dOp + (int64_t)q * bp.do_sn + ch * EPC);
@@ -317,7 +331,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i;
       const int off = lds_off<RB>(c / CPR, c % CPR);
-      *reinterpret_cast<uint4*>(base + off) = qst[i];
+      *reinterpret_cast<uint4*>(base + off) = ROPE ? rope_apply<T>(qst[i], qst_rc[i]) : qst[i];
       *reinterpret_cast<uint4*>(base + TILE + off) = dst[i];
     }
     if (tid < BQ) {
@@ -451,8 +465,10 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const AttnBwdParams bp
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d = dt * 32 + 8 * g + 4 * hh;
-        store4<T>(krow_dk + d, make_float4(dk[dt][4 * g] * sc, dk[dt][4 * g + 1] * sc, dk[dt][4 * g + 2] * sc,
-                                           dk[dt][4 * g + 3] * sc));
+        float v0 = dk[dt][4 * g] * sc, v1 = dk[dt][4 * g + 1] * sc, v2 = dk[dt][4 * g + 2] * sc,
+              v3 = dk[dt][4 * g + 3] * sc;
+        if (ROPE) rope_inv4(v0, v1, v2, v3, rope, kpos, d);  // dK w.r.t. the un-rotated k
+        store4<T>(krow_dk + d, make_float4(v0, v1, v2, v3));
         store4<T>(krow_dv + d, make_float4(dv[dt][4 * g], dv[dt][4 * g + 1], dv[dt][4 * g + 2], dv[dt][4 * g + 3]));
       }
   }
@@ -464,13 +480,16 @@ void launch_bwd(const AttnBwdParams& bp, hipStream_t s) {
   const int nqb = (p.Nq + 127) / 128;
   const int nkb = (p.Nk + 127) / 128;
   const dim3 gq((unsigned)(nqb * p.B * p.H)), gk((unsigned)(nkb * p.B * p.H)), block(256);
-  if (p.causal) {
-    hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, true>), gq, block, 0, s, bp);
-    hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, true>), gk, block, 0, s, bp);
-  } else {
-    hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, false>), gq, block, 0, s, bp);
-    hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, false>), gk, block, 0, s, bp);
-  }
+  auto go = [&](auto causal, auto rope) {
+    constexpr bool C = decltype(causal)::value, R = decltype(rope)::value;
+    hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, C, R>), gq, block, 0, s, bp);
+    hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, C, R>), gk, block, 0, s, bp);
+  };
+  const bool rope = p.rope_cos != nullptr;
+  if (p.causal && rope) go(std::true_type{}, std::true_type{});
+  else if (p.causal) go(std::true_type{}, std::false_type{});
+  else if (rope) go(std::false_type{}, std::true_type{});
+  else go(std::false_type{}, std::false_type{});
 }
 
 template <typename T>

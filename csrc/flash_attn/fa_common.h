@@ -152,6 +152,99 @@ __device__ __forceinline__ float lds_f1(const char* img, int r, int e) {
   return *reinterpret_cast<const float*>(img + lds_off<RB>(r, e >> 2) + ((e & 3) << 2));
 }
 
+// ---- fused RoPE (interleaved pairs) on 16-byte chunks ---------------------------------------
+// Rotation R(pos) of the pairs (d0, d0+1), ... of one chunk, computed in fp32 from the (ctx, D/2)
+// cos/sin cache (L2-resident); sgn = -1 applies R^T (the backward's inverse rotation).
+struct Rope {
+  const float* cs;
+  const float* sn;
+  int half;
+};
+
+template <typename T>
+__device__ __forceinline__ uint4 rope_chunk(uint4 u, const Rope& r, int64_t pos, int d0, float sgn) {
+  typedef typename Elem<T>::storage S;
+  if constexpr (sizeof(S) == 4) {
+    const float2 c = *reinterpret_cast<const float2*>(r.cs + pos * r.half + (d0 >> 1));
+    const float2 s = *reinterpret_cast<const float2*>(r.sn + pos * r.half + (d0 >> 1));
+    float4 v = __builtin_bit_cast(float4, u);
+    const float s0 = sgn * s.x, s1 = sgn * s.y;
+    float4 o;
+    o.x = c.x * v.x - s0 * v.y;
+    o.y = s0 * v.x + c.x * v.y;
+    o.z = c.y * v.z - s1 * v.w;
+    o.w = s1 * v.z + c.y * v.w;
+    return __builtin_bit_cast(uint4, o);
+  } else {
+    const float4 c = *reinterpret_cast<const float4*>(r.cs + pos * r.half + (d0 >> 1));
+    const float4 s = *reinterpret_cast<const float4*>(r.sn + pos * r.half + (d0 >> 1));
+    const float cc[4] = {c.x, c.y, c.z, c.w};
+    const float ss[4] = {sgn * s.x, sgn * s.y, sgn * s.z, sgn * s.w};
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float a = Elem<T>::to_f((S)(w[i] & 0xffff)), b = Elem<T>::to_f((S)(w[i] >> 16));
+      const float x = cc[i] * a - ss[i] * b, y = ss[i] * a + cc[i] * b;
+      w[i] = (uint32_t)Elem<T>::from_f(x) | ((uint32_t)Elem<T>::from_f(y) << 16);
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// Split form for software-pipelined staging: fetch the coefficients together with the tile's
+// global loads (no use of the loaded data yet), rotate when the registers are written to LDS.
+struct RopeCoef {
+  float4 c, s;
+};
+template <typename T>
+__device__ __forceinline__ RopeCoef rope_coef(const Rope& r, int64_t pos, int d0) {
+  RopeCoef k;
+  if constexpr (sizeof(typename Elem<T>::storage) == 4) {
+    const float2 c = *reinterpret_cast<const float2*>(r.cs + pos * r.half + (d0 >> 1));
+    const float2 s = *reinterpret_cast<const float2*>(r.sn + pos * r.half + (d0 >> 1));
+    k.c = make_float4(c.x, c.y, 0.f, 0.f);
+    k.s = make_float4(s.x, s.y, 0.f, 0.f);
+  } else {
+    k.c = *reinterpret_cast<const float4*>(r.cs + pos * r.half + (d0 >> 1));
+    k.s = *reinterpret_cast<const float4*>(r.sn + pos * r.half + (d0 >> 1));
+  }
+  return k;
+}
+template <typename T>
+__device__ __forceinline__ uint4 rope_apply(uint4 u, const RopeCoef& k) {
+  typedef typename Elem<T>::storage S;
+  if constexpr (sizeof(S) == 4) {
+    float4 v = __builtin_bit_cast(float4, u);
+    float4 o;
+    o.x = k.c.x * v.x - k.s.x * v.y;
+    o.y = k.s.x * v.x + k.c.x * v.y;
+    o.z = k.c.y * v.z - k.s.y * v.w;
+    o.w = k.s.y * v.z + k.c.y * v.w;
+    return __builtin_bit_cast(uint4, o);
+  } else {
+    const float cc[4] = {k.c.x, k.c.y, k.c.z, k.c.w};
+    const float ss[4] = {k.s.x, k.s.y, k.s.z, k.s.w};
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float a = Elem<T>::to_f((S)(w[i] & 0xffff)), b = Elem<T>::to_f((S)(w[i] >> 16));
+      const float x = cc[i] * a - ss[i] * b, y = ss[i] * a + cc[i] * b;
+      w[i] = (uint32_t)Elem<T>::from_f(x) | ((uint32_t)Elem<T>::from_f(y) << 16);
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// inverse rotation of 4 consecutive fp32 accumulator values (d0 % 4 == 0) before the dQ/dK store
+__device__ __forceinline__ void rope_inv4(float& v0, float& v1, float& v2, float& v3, const Rope& r, int64_t pos,
+                                          int d0) {
+  const float2 c = *reinterpret_cast<const float2*>(r.cs + pos * r.half + (d0 >> 1));
+  const float2 s = *reinterpret_cast<const float2*>(r.sn + pos * r.half + (d0 >> 1));
+  const float a0 = c.x * v0 + s.x * v1, a1 = -s.x * v0 + c.x * v1;
+  const float b0 = c.y * v2 + s.y * v3, b1 = -s.y * v2 + c.y * v3;
+  v0 = a0; v1 = a1; v2 = b0; v3 = b1;
+}
+
 // key (or row) index held by accumulator register `reg` of lane-half h in a 32x32 tile
 __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 

@@ -19,7 +19,7 @@
 namespace cs336 {
 namespace fa {
 
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, bool ROPE>
 __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
   typedef typename Elem<T>::storage S;
   constexpr bool F32 = std::is_same<T, float>::value;
@@ -58,24 +58,29 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
 
   // ---- Q fragments (B operand), resident for the whole kernel -------------------------------
   constexpr int NQF = F32 ? D / 8 : D / 16;  // uint4 per lane
+  const Rope rope{p.rope_cos, p.rope_sin, D / 2};
+  const int64_t* rpos = p.rope_pos ? p.rope_pos + (int64_t)b * p.Nq : nullptr;
   uint4 qf[NQF];
 #pragma unroll
   for (int i = 0; i < NQF; ++i) {
     // 16-bit: chunk 2*ks + hh  |  f32: d = hh*D/2 + 4*i .. +3
     const int e = F32 ? (hh * (D / 2) + 4 * i) : (16 * i + 8 * hh);
     qf[i] = valid_q ? *reinterpret_cast<const uint4*>(Qp + (int64_t)qrow * p.q_sn + e) : make_uint4(0, 0, 0, 0);
+    if (ROPE && valid_q) qf[i] = rope_chunk<T>(qf[i], rope, rpos ? rpos[qrow] : qrow, e, 1.f);
   }
 
   const int kv_end = CAUSAL ? min(p.Nk, q0 + BM) : p.Nk;
   const int ntiles = (kv_end + BN - 1) / BN;
 
   uint4 kst[LPT], vst[LPT];
+  RopeCoef kst_rc[ROPE ? LPT : 1];  // rotation applied at LDS-write time (keeps the prefetch async)
   auto gload = [&](int j) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i;
       const int r = c / CPR, ch = c % CPR;
       const int key = j * BN + r;
+      if (ROPE) kst_rc[i] = rope_coef<T>(rope, key < p.Nk ? (rpos ? rpos[key] : key) : 0, ch * EPC);
       if (key < p.Nk) {
         kst[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)key * p.k_sn + ch * EPC);
         vst[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)key * p.v_sn + ch * EPC);
@@ -92,7 +97,7 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
       const int c = tid + 256 * i;
       const int r = c / CPR, ch = c % CPR;
       const int off = lds_off<RB>(r, ch);
-      *reinterpret_cast<uint4*>(Ks + off) = kst[i];
+      *reinterpret_cast<uint4*>(Ks + off) = ROPE ? rope_apply<T>(kst[i], kst_rc[i]) : kst[i];
       *reinterpret_cast<uint4*>(Ks + TILE + off) = vst[i];
     }
   };
@@ -235,8 +240,11 @@ template <typename T, int D>
 void launch_fwd(const AttnParams& p, hipStream_t s) {
   const int nqb = (p.Nq + 127) / 128;
   const dim3 grid((unsigned)(nqb * p.B * p.H)), block(256);
-  if (p.causal) hipLaunchKernelGGL((fa_fwd_kernel<T, D, true>), grid, block, 0, s, p);
-  else hipLaunchKernelGGL((fa_fwd_kernel<T, D, false>), grid, block, 0, s, p);
+  const bool rope = p.rope_cos != nullptr;
+  if (p.causal && rope) hipLaunchKernelGGL((fa_fwd_kernel<T, D, true, true>), grid, block, 0, s, p);
+  else if (p.causal) hipLaunchKernelGGL((fa_fwd_kernel<T, D, true, false>), grid, block, 0, s, p);
+  else if (rope) hipLaunchKernelGGL((fa_fwd_kernel<T, D, false, true>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((fa_fwd_kernel<T, D, false, false>), grid, block, 0, s, p);
 }
 
 template <typename T>

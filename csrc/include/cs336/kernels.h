@@ -77,6 +77,11 @@ struct AttnParams {
   int B, H, Nq, Nk, D;
   float scale;
   bool causal;
+  // optional fused RoPE on q and k (self-attention, Nq == Nk): cos/sin (ctx, D/2) fp32, positions
+  // (B, N) int64 or nullptr (= index). q/k are the UN-rotated projections; dq/dk come out un-rotated.
+  const float* rope_cos = nullptr;
+  const float* rope_sin = nullptr;
+  const int64_t* rope_pos = nullptr;
 };
 
 struct AttnBwdParams {
