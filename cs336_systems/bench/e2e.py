@@ -128,8 +128,10 @@ def run_memory_profile(size: str, context_length: int, mode: str = "fullstep", m
     reset_peak(dev)
     with record_memory_history(snapshot):
         if mode == "forward":
-            with torch.no_grad(), ctx:
-                model(x)
+            # grad mode on, as in the reference: the live logits keep every saved activation
+            with ctx:
+                logits = model(x)
+            del logits
         else:
             with ctx:
                 loss = ops.cross_entropy(model(x), y)
