@@ -1,0 +1,214 @@
+"""Data-parallel Transformer-LM training driver with checkpoint/resume.
+
+The reference trains through ad-hoc scripts with hard-coded hparams
+(``ddp_bucketed_overlapped_sharded.py:367-404``, ``naive_ddp.py:662-684``) and cannot resume.
+This driver is one torchrun-compatible entry point over the framework's pieces:
+
+* model: :func:`cs336_systems.models.build_model` (registry size or explicit dims), bf16 autocast
+  over fp32 master weights, HIP kernels on GPU;
+* data parallelism: any of the four DP variants (``--ddp``) and optional ZeRO-1 (``--sharded``);
+* optimizer: fused HIP AdamW (bf16 weight shadows on GPU), cosine LR with warmup, global-norm
+  clipping;
+* data: a 1-D token file (``.npy`` or raw ``uint16`` ``.bin``, memory-mapped) or synthetic tokens;
+  batch ``s`` is drawn from a generator seeded by ``(seed, s)``, identical on every rank (each rank
+  takes its slice), so a resumed run replays exactly the batches the uninterrupted run would have;
+* checkpoints: :mod:`cs336_systems.checkpoint` every ``--ckpt-every`` steps and at the end;
+  ``--resume`` continues from ``<ckpt-dir>/latest``;
+* failure handling: process-group timeout + async error handling (``setup_distributed``), a
+  non-finite loss aborts the job (no checkpoint is written over a good one).
+
+Usage::
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m cs336_systems.train --size xl --ctx 512 \
+        --batch 192 --steps 1000 --ddp bucketed --ckpt-dir ckpt/ --resume
+"""
+
+from __future__ import annotations
+
+import argparse
+import contextlib
+import dataclasses
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
+from .models import build_model
+from .models.fused import refresh_bf16_shadows
+from .parallel import DEFAULT_BUCKET_MB, ShardedOptimizer, cleanup_distributed, setup_distributed, wrap_ddp
+
+
+@dataclasses.dataclass
+class TrainConfig:
+    size: str = "small"
+    ctx: int = 256
+    vocab: int = 10000
+    batch: int = 8  # global batch (sequences), split over ranks
+    steps: int = 100
+    lr: float = 3e-4
+    min_lr: float = 3e-5
+    warmup: int = 10
+    wd: float = 0.1
+    beta1: float = 0.9
+    beta2: float = 0.95
+    eps: float = 1e-8
+    clip: float = 1.0
+    dtype: str = "bf16"  # autocast dtype on GPU; "fp32" disables autocast
+    ddp: str = "bucketed"
+    bucket_mb: float = DEFAULT_BUCKET_MB
+    sharded: bool = False
+    data: str | None = None  # token file; None = synthetic
+    seed: int = 0
+    ckpt_dir: str | None = None
+    ckpt_every: int = 0
+    resume: bool = False
+    stop_after: int = 0  # run at most this many steps in this invocation, checkpoint, exit (0 = all)
+    log_every: int = 10
+    log_file: str | None = None
+    device: str = "auto"  # auto | cuda | cpu
+
+
+def lr_at(step: int, cfg: TrainConfig) -> float:
+    """Linear warmup then cosine decay to ``min_lr`` at ``steps`` (``cs336_basics.get_cosine_lr``)."""
+    if step < cfg.warmup:
+        return cfg.lr * step / max(1, cfg.warmup)
+    if step >= cfg.steps:
+        return cfg.min_lr
+    frac = (step - cfg.warmup) / max(1, cfg.steps - cfg.warmup)
+    return cfg.min_lr + 0.5 * (1 + math.cos(math.pi * frac)) * (cfg.lr - cfg.min_lr)
+
+
+def open_tokens(path: str) -> np.ndarray:
+    if path.endswith(".npy"):
+        return np.load(path, mmap_mode="r", allow_pickle=False)
+    return np.memmap(path, dtype=np.uint16, mode="r")
+
+
+class Batches:
+    """Deterministic per-step batches: global batch ``s`` depends only on ``(seed, s)``."""
+
+    def __init__(self, cfg: TrainConfig, rank: int, world: int, device: torch.device):
+        if cfg.batch % world:
+            raise ValueError(f"global batch {cfg.batch} must divide by world size {world}")
+        self.cfg, self.rank, self.local, self.device = cfg, rank, cfg.batch // world, device
+        self.tokens = open_tokens(cfg.data) if cfg.data else None
+
+    def __call__(self, step: int) -> tuple[torch.Tensor, torch.Tensor]:
+        cfg = self.cfg
+        g = torch.Generator().manual_seed(cfg.seed * 1_000_003 + step)
+        lo, hi = self.rank * self.local, (self.rank + 1) * self.local
+        if self.tokens is None:
+            toks = torch.randint(0, cfg.vocab, (cfg.batch, cfg.ctx + 1), generator=g)[lo:hi]
+        else:
+            starts = torch.randint(0, len(self.tokens) - cfg.ctx - 1, (cfg.batch,), generator=g)[lo:hi].numpy()
+            idx = starts[:, None] + np.arange(cfg.ctx + 1)[None, :]
+            toks = torch.from_numpy(np.asarray(self.tokens[idx]).astype(np.int64))
+        if self.device.type == "cuda":
+            toks = toks.pin_memory().to(self.device, non_blocking=True)
+        return toks[:, :-1].contiguous(), toks[:, 1:].contiguous()
+
+
+def train(cfg: TrainConfig) -> dict:
+    use_cuda = cfg.device == "cuda" or (cfg.device == "auto" and torch.cuda.is_available())
+    rank, world, dev = setup_distributed(backend="nccl" if use_cuda else "gloo")
+    torch.manual_seed(cfg.seed)
+    model = build_model(cfg.size, cfg.ctx, vocab_size=cfg.vocab, device=dev)
+    okw = dict(lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.eps, weight_decay=cfg.wd)
+    shadows = dev.type == "cuda" and cfg.dtype == "bf16"
+    if cfg.sharded:
+        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, **okw)
+    else:
+        opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)
+
+    start = 0
+    if cfg.resume and cfg.ckpt_dir:
+        path = latest_checkpoint(cfg.ckpt_dir)
+        if path is not None:
+            meta = load_checkpoint(path, model, opt, map_location=dev)
+            start = int(meta["step"])
+            refresh_bf16_shadows(model.parameters())
+            if rank == 0:
+                print(f"resumed from {path} at step {start}", flush=True)
+    # DDP wraps after loading so its initial broadcast ships the restored weights
+    ddp = wrap_ddp(model, cfg.ddp, bucket_size_mb=cfg.bucket_mb)
+    batches = Batches(cfg, rank, world, dev)
+    amp = dev.type == "cuda" and cfg.dtype == "bf16"
+    autocast = (lambda: torch.autocast("cuda", dtype=torch.bfloat16)) if amp else contextlib.nullcontext
+    log = open(cfg.log_file, "a") if (cfg.log_file and rank == 0) else None
+    hist = []
+    t_last, tok_since = time.perf_counter(), 0
+    loss_val = float("nan")
+    end = min(cfg.steps, start + cfg.stop_after) if cfg.stop_after > 0 else cfg.steps
+    for step in range(start, end):
+        lr = lr_at(step, cfg)
+        for g in opt.param_groups:
+            g["lr"] = lr
+        x, y = batches(step)
+        if hasattr(ddp, "zero_grad") and cfg.ddp in ("bucketed", "flat"):
+            ddp.zero_grad()
+        else:
+            opt.zero_grad(set_to_none=True)
+        with autocast():
+            loss = ops.cross_entropy(ddp(x), y)
+        loss.backward()
+        ddp.finish_gradient_synchronization()
+        gnorm = ops.clip_grad_norm_(model.parameters(), cfg.clip) if cfg.clip > 0 else None
+        opt.step()
+        tok_since += cfg.batch * cfg.ctx
+        done = step + 1
+        if done % cfg.log_every == 0 or done == end:
+            lt = loss.detach().float().clone()
+            dist.all_reduce(lt)
+            loss_val = float(lt) / world
+            if not math.isfinite(loss_val):
+                raise FloatingPointError(f"non-finite loss {loss_val} at step {done}; not checkpointing")
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            now = time.perf_counter()
+            rec = dict(step=done, loss=loss_val, lr=lr, tokens_per_s=tok_since / (now - t_last))
+            if gnorm is not None:
+                rec["grad_norm"] = float(gnorm)
+            t_last, tok_since = now, 0
+            hist.append(rec)
+            if rank == 0:
+                print(json.dumps(rec), flush=True)
+                if log:
+                    log.write(json.dumps(rec) + "\n")
+                    log.flush()
+        if cfg.ckpt_dir and ((cfg.ckpt_every and done % cfg.ckpt_every == 0) or done == end):
+            save_checkpoint(cfg.ckpt_dir, done, model, opt, meta=dict(config=dataclasses.asdict(cfg)))
+    if log:
+        log.close()
+    return dict(rank=rank, world=world, start=start, history=hist, final_loss=loss_val)
+
+
+def parse(argv=None) -> TrainConfig:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    for f in dataclasses.fields(TrainConfig):
+        name = "--" + f.name.replace("_", "-")
+        if f.type in ("bool", bool):
+            ap.add_argument(name, action="store_true", default=f.default)
+        else:
+            typ = {"int": int, "float": float}.get(str(f.type), str)
+            ap.add_argument(name, type=typ, default=f.default)
+    return TrainConfig(**vars(ap.parse_args(argv)))
+
+
+def main(argv=None) -> int:
+    cfg = parse(argv)
+    try:
+        train(cfg)
+    finally:
+        cleanup_distributed()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
