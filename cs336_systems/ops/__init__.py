@@ -11,7 +11,7 @@ from .flash_attention import (
     flash_attention,
     naive_attention,
 )
-from .rmsnorm import rmsnorm, rmsnorm_ref
+from .rmsnorm import add_rmsnorm, add_rmsnorm_ref, rmsnorm, rmsnorm_ref
 from .rope import rope, rope_ref
 from .swiglu import silu, silu_mul, silu_mul_ref
 
@@ -33,6 +33,8 @@ __all__ = [
     "FlashAttentionTriton",
     "flash_attention",
     "naive_attention",
+    "add_rmsnorm",
+    "add_rmsnorm_ref",
     "rmsnorm",
     "rmsnorm_ref",
     "rope",

@@ -33,6 +33,17 @@ def _rms_bwd(dy, x, w, rstd):
     return torch.empty_like(x), w.new_empty(w.shape, dtype=torch.float32)
 
 
+@register_fake("cs336::add_rmsnorm_fwd")
+def _add_rms_fwd(x, r, w, eps, out_dtype):
+    return torch.empty_like(x), x.new_empty(x.shape, dtype=out_dtype or x.dtype), x.new_empty((x.shape[0],), dtype=torch.float32)
+
+
+@register_fake("cs336::rmsnorm_bwd_add")
+def _rms_bwd_add(dy, x, w, rstd, dres, emit_bf16):
+    dx2 = x.new_empty(x.shape if emit_bf16 else (0,), dtype=torch.bfloat16)
+    return torch.empty_like(x), dx2, w.new_empty(w.shape, dtype=torch.float32)
+
+
 @register_fake("cs336::rope")
 def _rope(x, cos, sin, pos, inverse):
     return _bnhd_like(x)

@@ -45,6 +45,73 @@ class RMSNormHIP(torch.autograd.Function):
         return dx.view(ctx.shape), dw.to(weight.dtype), None, None
 
 
+class AddRMSNormHIP(torch.autograd.Function):
+    """``s = x + r; y = rmsnorm(s)`` in one pass; backward ``ds = rmsnorm_bwd(dy) + ds_next`` in one
+    pass, emitting the bf16 copy of ``ds`` for a bf16 branch ``r`` from the same kernel."""
+
+    @staticmethod
+    def forward(ctx, x, r, weight, eps, out_dtype):
+        shape = x.shape
+        s, y, rstd = ops().add_rmsnorm_fwd(x.reshape(-1, shape[-1]), r.reshape(-1, shape[-1]), weight, eps, out_dtype)
+        ctx.save_for_backward(s, weight, rstd)
+        ctx.shape, ctx.r_dtype = shape, r.dtype
+        return s.view(shape), y.view(*shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        s, weight, rstd = ctx.saved_tensors
+        H = ctx.shape[-1]
+        if dy is None:
+            dx = ds
+            dw = torch.zeros_like(weight)
+            dr = ds.to(ctx.r_dtype)
+            return dx, dr, dw, None, None
+        dy2 = dy.reshape(-1, H)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        if ds is None:
+            dx, dw = ops().rmsnorm_bwd(dy2, s, weight, rstd)
+            dr = dx if ctx.r_dtype == dx.dtype else dx.to(ctx.r_dtype)
+        else:
+            ds2 = ds.reshape(-1, H)
+            if not ds2.is_contiguous() or ds2.dtype != s.dtype:
+                ds2 = ds2.contiguous().to(s.dtype)
+            emit = ctx.r_dtype == torch.bfloat16 and s.dtype != torch.bfloat16
+            dx, dx_bf16, dw = ops().rmsnorm_bwd_add(dy2, s, weight, rstd, ds2, emit)
+            dr = dx_bf16 if emit else (dx if ctx.r_dtype == dx.dtype else dx.to(ctx.r_dtype))
+        return dx.view(ctx.shape), dr.view(ctx.shape), dw.to(weight.dtype), None, None
+
+
+def add_rmsnorm_ref(x, r, weight, eps=1e-5):
+    s = x + r
+    return s, rmsnorm_ref(s, weight, eps)
+
+
+def add_rmsnorm(x: torch.Tensor, r: torch.Tensor, weight: torch.Tensor, eps: float = 1e-5, out_dtype: torch.dtype | None = None):
+    """Pre-norm residual step: returns ``(s, rmsnorm(s))`` with ``s = x + r`` (reference
+    ``model.py:380-386`` does the add and the next block's norm as two ops)."""
+    H = x.shape[-1]
+    if (
+        H % 4 == 0
+        and H <= 8192
+        and use_hip(x)
+        and weight.dtype == torch.float32
+        and x.dtype in (torch.float32, torch.bfloat16)
+        and r.dtype in (torch.float32, torch.bfloat16)
+        and x.shape == r.shape
+        and torch.result_type(x, r) == x.dtype
+    ):
+        if out_dtype is None:
+            out_dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+        if not x.is_contiguous():
+            x = x.contiguous()
+        if not r.is_contiguous():
+            r = r.contiguous()
+        return AddRMSNormHIP.apply(x, r, weight, eps, out_dtype)
+    s = x + r
+    return s, rmsnorm(s, weight, eps, out_dtype)
+
+
 def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-5, out_dtype: torch.dtype | None = None):
     """RMSNorm over the last dim. ``out_dtype`` defaults to the autocast dtype when autocast is on
     (the consumer is a GEMM that would cast anyway), else the input dtype."""

@@ -216,6 +216,57 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
   return {dx, dw};
 }
 
+static bool f32_or_bf16(const at::Tensor& t) {
+  return t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16;
+}
+
+// s = x + r; y = rmsnorm(s) * w  (pre-norm residual add fused with the next norm)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> add_rmsnorm_fwd(const at::Tensor& x, const at::Tensor& r,
+                                                               const at::Tensor& w, double eps,
+                                                               std::optional<at::ScalarType> out_dtype) {
+  check_cuda(x, "x");
+  check_cuda(r, "r");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && r.is_contiguous() && r.sizes() == x.sizes(),
+              "cs336: add_rmsnorm x, r must be contiguous (M, H) of the same shape");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == x.size(1),
+              "cs336: add_rmsnorm weight must be fp32 (H)");
+  TORCH_CHECK(f32_or_bf16(x) && f32_or_bf16(r), "cs336: add_rmsnorm x, r must be fp32 or bf16");
+  TORCH_CHECK(x.size(1) % 4 == 0 && x.size(1) <= 8192, "cs336: rmsnorm hidden size must be a multiple of 4, <= 8192");
+  c10::DeviceGuard g(x.device());
+  at::Tensor y = at::empty_like(x, x.options().dtype(out_dtype.value_or(x.scalar_type())));
+  TORCH_CHECK(f32_or_bf16(y), "cs336: add_rmsnorm out dtype must be fp32 or bf16");
+  at::Tensor s = at::empty_like(x);
+  at::Tensor rstd = at::empty({x.size(0)}, x.options().dtype(at::kFloat));
+  if (x.size(0) == 0) return {s, y, rstd};
+  cs336::add_rmsnorm_fwd(x.data_ptr(), to_dtype(x), r.data_ptr(), to_dtype(r), w.data_ptr<float>(), y.data_ptr(),
+                         to_dtype(y), s.data_ptr(), rstd.data_ptr<float>(), x.size(0), x.size(1), (float)eps, stream());
+  return {s, y, rstd};
+}
+
+// dx = rmsnorm_bwd(dy; s) + dres; dx_bf16 = bf16(dx) when emit_bf16 (else an empty tensor)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add(const at::Tensor& dy, const at::Tensor& x,
+                                                               const at::Tensor& w, const at::Tensor& rstd,
+                                                               const at::Tensor& dres, bool emit_bf16) {
+  check_cuda(dy, "dy");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "cs336: rmsnorm_bwd_add shapes");
+  TORCH_CHECK(dres.is_contiguous() && dres.sizes() == x.sizes() && dres.scalar_type() == x.scalar_type(),
+              "cs336: rmsnorm_bwd_add dres must match x");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == x.size(1),
+              "cs336: rmsnorm_bwd_add weight must be fp32 (H)");
+  TORCH_CHECK(f32_or_bf16(dy) && f32_or_bf16(x), "cs336: rmsnorm_bwd_add dtypes must be fp32 or bf16");
+  c10::DeviceGuard g(x.device());
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dx2 = emit_bf16 ? at::empty_like(x, x.options().dtype(at::kBFloat16)) : at::empty({0}, x.options().dtype(at::kBFloat16));
+  if (x.size(0) == 0) return {dx, dx2, at::zeros({x.size(1)}, x.options().dtype(at::kFloat))};
+  at::Tensor dw = at::empty({x.size(1)}, x.options().dtype(at::kFloat));
+  const int rows = cs336::rmsnorm_bwd_workspace_rows(x.size(0), x.size(1));
+  at::Tensor ws = at::empty({(int64_t)rows, x.size(1)}, x.options().dtype(at::kFloat));
+  cs336::rmsnorm_bwd_add(dy.data_ptr(), to_dtype(dy), x.data_ptr(), to_dtype(x), w.data_ptr<float>(),
+                         rstd.data_ptr<float>(), dres.data_ptr(), dx.data_ptr(), emit_bf16 ? dx2.data_ptr() : nullptr,
+                         dw.data_ptr<float>(), ws.data_ptr<float>(), x.size(0), x.size(1), stream());
+  return {dx, dx2, dw};
+}
+
 // ------------------------------------------------------------------------------------------
 // RoPE
 // ------------------------------------------------------------------------------------------
@@ -441,6 +492,8 @@ TORCH_LIBRARY(cs336, m) {
       "(Tensor, Tensor, Tensor)");
   m.def("rmsnorm_fwd(Tensor x, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
+  m.def("add_rmsnorm_fwd(Tensor x, Tensor r, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor, Tensor)");
+  m.def("rmsnorm_bwd_add(Tensor dy, Tensor x, Tensor weight, Tensor rstd, Tensor dres, bool emit_bf16) -> (Tensor, Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, Tensor? pos, bool inverse) -> Tensor");
   m.def(
       "fa_bwd_into(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale, "
@@ -465,6 +518,8 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("fa_bwd", &fa_bwd);
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+  m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
+  m.impl("rmsnorm_bwd_add", &rmsnorm_bwd_add);
   m.impl("rope", &rope);
   m.impl("fa_bwd_into", &fa_bwd_into);
   m.impl("rope_into", &rope_into);

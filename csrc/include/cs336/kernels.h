@@ -16,6 +16,13 @@ void rmsnorm_fwd(const void* x, DType xt, const void* w, DType wt, void* y, DTyp
 void rmsnorm_bwd(const void* dy, DType dyt, const void* x, DType xt, const void* w, DType wt, const float* rstd,
                  void* dx, float* dw, float* workspace, int64_t M, int64_t H, hipStream_t s);
 int rmsnorm_bwd_workspace_rows(int64_t M, int64_t H);
+// fused pre-norm residual: sum = x + r (dtype xt), y = rmsnorm(sum) * w; xt/rt/yt in {F32, BF16}
+void add_rmsnorm_fwd(const void* x, DType xt, const void* r, DType rt, const float* w, void* y, DType yt, void* sum,
+                     float* rstd, int64_t M, int64_t H, float eps, hipStream_t s);
+// dx = rmsnorm_bwd(dy) + dres (dtype xt, dres same dtype); dx_bf16 (optional) = bf16 copy of dx
+void rmsnorm_bwd_add(const void* dy, DType dyt, const void* x, DType xt, const float* w, const float* rstd,
+                     const void* dres, void* dx, void* dx_bf16, float* dw, float* workspace, int64_t M, int64_t H,
+                     hipStream_t s);
 
 // ---- RoPE (csrc/ops/rope.hip) ----
 // x: (B,H,N,D) strided (elements), out: contiguous (B,N,H,D); cos/sin: (ctx, D/2) fp32;

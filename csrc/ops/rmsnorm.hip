@@ -15,11 +15,15 @@
 namespace cs336 {
 namespace {
 
-template <typename TX, typename TW, typename TY, int NV>
+// ADD: s = x + r is formed in fp32, stored (dtype TX: the residual stream) and normalized, so the
+// residual add of a pre-norm block and the next RMSNorm read the stream once instead of twice.
+template <typename TX, typename TW, typename TY, int NV, bool ADD = false, typename TR = TX>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const typename Elem<TX>::storage* __restrict__ x,
                                                           const typename Elem<TW>::storage* __restrict__ w,
                                                           typename Elem<TY>::storage* __restrict__ y,
-                                                          float* __restrict__ rstd, int64_t M, int H, float eps) {
+                                                          float* __restrict__ rstd, int64_t M, int H, float eps,
+                                                          const typename Elem<TR>::storage* __restrict__ res = nullptr,
+                                                          typename Elem<TX>::storage* __restrict__ s = nullptr) {
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int64_t row = (int64_t)blockIdx.x * 4 + wave;
   if (row >= M) return;
@@ -32,6 +36,18 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const typename Elem<TX
     const int i = lane + kWave * k;
     if (i < H4) {
       v[k] = load4<TX>(xr + 4 * i);
+      if constexpr (ADD) {
+        const float4 rv = load4<TR>(res + row * H + 4 * i);
+        v[k].x += rv.x; v[k].y += rv.y; v[k].z += rv.z; v[k].w += rv.w;
+        store4<TX>(s + row * H + 4 * i, v[k]);
+        // normalize what was stored (rounded to TX), like the unfused add -> rmsnorm
+        if constexpr (!std::is_same<TX, float>::value) {
+          v[k].x = Elem<TX>::to_f(Elem<TX>::from_f(v[k].x));
+          v[k].y = Elem<TX>::to_f(Elem<TX>::from_f(v[k].y));
+          v[k].z = Elem<TX>::to_f(Elem<TX>::from_f(v[k].z));
+          v[k].w = Elem<TX>::to_f(Elem<TX>::from_f(v[k].w));
+        }
+      }
       ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
     } else {
       v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -56,13 +72,17 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const typename Elem<TX
   }
 }
 
-template <typename TDY, typename TX, typename TW, int NV>
+// ADD: dx += dres (the gradient that reaches the residual stream from later layers) and, if dx2 is
+// given, a bf16 copy of the sum for the branch whose output was bf16 (the o/w2 projection GEMM).
+template <typename TDY, typename TX, typename TW, int NV, bool ADD = false>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const typename Elem<TDY>::storage* __restrict__ dy,
                                                           const typename Elem<TX>::storage* __restrict__ x,
                                                           const typename Elem<TW>::storage* __restrict__ w,
                                                           const float* __restrict__ rstd,
                                                           typename Elem<TX>::storage* __restrict__ dx,
-                                                          float* __restrict__ ws, int64_t M, int H) {
+                                                          float* __restrict__ ws, int64_t M, int H,
+                                                          const typename Elem<TX>::storage* __restrict__ dres = nullptr,
+                                                          bf16_t* __restrict__ dx2 = nullptr) {
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int H4 = H >> 2;
   const int64_t nw = (int64_t)gridDim.x * 4;
@@ -105,6 +125,11 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const typename Elem<TD
         o.y = r * wv[k].y * gv[k].y - c * xv[k].y;
         o.z = r * wv[k].z * gv[k].z - c * xv[k].z;
         o.w = r * wv[k].w * gv[k].w - c * xv[k].w;
+        if constexpr (ADD) {
+          const float4 d = load4<TX>(dres + row * H + 4 * i);
+          o.x += d.x; o.y += d.y; o.z += d.z; o.w += d.w;
+          if (dx2) store4<BF16>(dx2 + row * H + 4 * i, o);
+        }
         store4<TX>(dxr + 4 * i, o);
         dwp[k].x += gv[k].x * xv[k].x * r;
         dwp[k].y += gv[k].y * xv[k].y * r;
@@ -224,6 +249,57 @@ void rmsnorm_bwd(const void* dy, DType dyt, const void* x, DType xt, const void*
                              (const typename Elem<TW>::storage*)w, rstd, (typename Elem<TX>::storage*)dx, workspace,
                              M, (int)H);
         });
+      });
+    });
+  });
+  float* split = workspace + (int64_t)nb * H;
+  const unsigned ct = (unsigned)((H + 255) / 256);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ct, kColSplits), dim3(256), 0, s, workspace, split, nb, (int)H);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ct, 1), dim3(256), 0, s, split, dw, kColSplits, (int)H);
+}
+
+// Fused residual variants: fp32 weights only (master weights), stream/branch dtypes fp32 or bf16.
+template <typename F>
+void dispatch_f32_bf16(DType t, F&& f) {
+  if (t == DType::F32) f(float{});
+  else f(BF16{});
+}
+
+void add_rmsnorm_fwd(const void* x, DType xt, const void* r, DType rt, const float* w, void* y, DType yt, void* sum,
+                     float* rstd, int64_t M, int64_t H, float eps, hipStream_t s) {
+  const dim3 grid((unsigned)((M + 3) / 4)), block(256);
+  dispatch_nv<0>((int)H, [&](auto nv) {
+    constexpr int NV = decltype(nv)::value;
+    dispatch_f32_bf16(xt, [&](auto tx) {
+      using TX = decltype(tx);
+      dispatch_f32_bf16(rt, [&](auto tr) {
+        using TR = decltype(tr);
+        dispatch_f32_bf16(yt, [&](auto ty) {
+          using TY = decltype(ty);
+          hipLaunchKernelGGL((rmsnorm_fwd_kernel<TX, float, TY, NV, true, TR>), grid, block, 0, s,
+                             (const typename Elem<TX>::storage*)x, w, (typename Elem<TY>::storage*)y, rstd, M, (int)H,
+                             eps, (const typename Elem<TR>::storage*)r, (typename Elem<TX>::storage*)sum);
+        });
+      });
+    });
+  });
+}
+
+void rmsnorm_bwd_add(const void* dy, DType dyt, const void* x, DType xt, const float* w, const float* rstd,
+                     const void* dres, void* dx, void* dx_bf16, float* dw, float* workspace, int64_t M, int64_t H,
+                     hipStream_t s) {
+  const int nb = bwd_blocks(M);
+  const size_t lds = (size_t)H * sizeof(float);
+  dispatch_nv<0>((int)H, [&](auto nv) {
+    constexpr int NV = decltype(nv)::value;
+    dispatch_f32_bf16(dyt, [&](auto tdy) {
+      using TDY = decltype(tdy);
+      dispatch_f32_bf16(xt, [&](auto tx) {
+        using TX = decltype(tx);
+        hipLaunchKernelGGL((rmsnorm_bwd_kernel<TDY, TX, float, NV, true>), dim3(nb), dim3(256), lds, s,
+                           (const typename Elem<TDY>::storage*)dy, (const typename Elem<TX>::storage*)x, w, rstd,
+                           (typename Elem<TX>::storage*)dx, workspace, M, (int)H,
+                           (const typename Elem<TX>::storage*)dres, (bf16_t*)dx_bf16);
       });
     });
   });
