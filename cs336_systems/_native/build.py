@@ -29,6 +29,9 @@ LIB = os.path.join(OUT_DIR, "libcs336_hip.so")
 ARCH = os.environ.get("CS336_OFFLOAD_ARCH", os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")).split(";")[0]
 
 
+VGPR_FORM = ("-mllvm", "-amdgpu-mfma-vgpr-form")
+
+
 def _torch_paths():
     import torch
 
@@ -82,7 +85,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
     # -amdgpu-mfma-vgpr-form: keep MFMA accumulators in arch VGPRs (gfx950's file is unified) instead
     # of AGPRs; otherwise hipcc copies every accumulator AGPR<->VGPR around each VALU touch
     # (online-softmax rescale), ~250 v_accvgpr moves per FA tile and half the occupancy.
-    kflags = common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result", "-mllvm", "-amdgpu-mfma-vgpr-form"]
+    kflags = common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result", *VGPR_FORM]
     if save_temps:
         kflags += ["-save-temps=obj"]
     hflags = common + ["-DUSE_ROCM", "-D__HIP_PLATFORM_AMD__"] + ["-I" + i for i in incs] + [f"--offload-arch={ARCH}"]
@@ -90,7 +93,11 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
     for src in kernels:
         obj = _obj_for(src)
         if force or _stale(src, obj, hdr_mtime):
-            jobs_list.append([hipcc, *kflags, "-c", src, "-o", obj])
+            with open(src) as fh:
+                # pure-MFMA kernels (GEMM) keep accumulators in AGPRs: no VALU touches them in the loop
+                agpr = "cs336-build: agpr-accumulators" in fh.read(4096)
+            flags = kflags if not agpr else [f for f in kflags if f not in VGPR_FORM]
+            jobs_list.append([hipcc, *flags, "-c", src, "-o", obj])
     for src in host:
         obj = _obj_for(src)
         if force or _stale(src, obj, hdr_mtime):

@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from ..ops import gemm
 from ..ops._ext import ops as _hip
 
 _SHADOW = "_cs336_bf16"
@@ -168,7 +169,7 @@ class FusedLinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         if x2.dtype != cdt:
             x2 = x2.to(cdt)
-        y = torch.mm(x2, w.t())
+        y = gemm.mm_nt(x2, w)
         ctx.save_for_backward(x2, w)
         ctx.x_shape = x.shape
         ctx.x_dtype = x.dtype
@@ -195,14 +196,15 @@ class FusedLinearFn(torch.autograd.Function):
             dy2 = dy2.to(w.dtype)
         dx = dw_parts = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, w).view(ctx.x_shape)
+            dx = gemm.mm_nn(dy2, w).view(ctx.x_shape)
             if dx.dtype != ctx.x_dtype:
                 dx = dx.to(ctx.x_dtype)
         if any(ctx.needs_input_grad[1:]):
             target = FusedLinearFn._grad_target(ctx.weights) if dy2.dtype == torch.bfloat16 else None
             if target is not None:
-                torch.mm(dy2.t(), x2, out_dtype=torch.float32, out=target)
-                dw = target
+                dw = gemm.mm_tn_fp32(dy2, x2, out=target)
+            elif dy2.dtype == torch.bfloat16 and dy2.is_cuda:
+                dw = gemm.mm_tn_fp32(dy2, x2)
             else:
                 dw = _mm_fp32_out(dy2.t(), x2)
             dw_parts = list(torch.split(dw, ctx.rows, 0))

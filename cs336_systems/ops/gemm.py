@@ -1,0 +1,55 @@
+"""Projection GEMMs: hipBLASLt (``torch.mm``) or the hand-written MFMA kernel (``csrc/gemm/gemm.hip``).
+
+``CS336_GEMM=hip`` routes every supported projection GEMM of :class:`FusedLinearFn` (forward
+``X·Wᵀ``, input-grad ``dY·W``, weight-grad ``dYᵀ·X`` with fp32 output, optionally straight into a
+DDP bucket) through the cs336 kernel; the default ``blas`` keeps hipBLASLt, which measured faster
+on the XL shapes in round 1 (``profiles/r1_gemm_cs336_vs_hipblaslt.json``: the cs336 kernel reaches
+60-100 % of hipBLASLt's TFLOPS; hipBLASLt picks stream-K 160×256 Tensile kernels for these shapes).
+Unsupported shapes (tile divisibility, K % 64) always fall back to ``torch.mm``.
+"""
+
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ._ext import ext_available, ops
+
+
+def hip_gemm_enabled() -> bool:
+    return os.environ.get("CS336_GEMM", "blas").lower() == "hip" and ext_available()
+
+
+def _ok(a, b, ta, tb) -> bool:
+    return a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and ops().gemm_ok(a, b, ta, tb)
+
+
+def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``x @ w.T`` (forward of a linear layer)."""
+    if hip_gemm_enabled() and _ok(x, w, False, True):
+        return ops().gemm(x, w, False, True, torch.bfloat16, 0, 0, 0)
+    return torch.mm(x, w.t())
+
+
+def mm_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``dy @ w`` (input gradient)."""
+    if hip_gemm_enabled() and _ok(dy, w, False, False):
+        return ops().gemm(dy, w, False, False, torch.bfloat16, 0, 0, 0)
+    return torch.mm(dy, w)
+
+
+def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``dy.T @ x`` with an fp32 result (weight gradient), written into ``out`` when given."""
+    if hip_gemm_enabled() and _ok(dy, x, True, False):
+        if out is not None:
+            ops().gemm_out(dy, x, True, False, out, False, 0, 0, 0)
+            return out
+        return ops().gemm(dy, x, True, False, torch.float32, 0, 0, 0)
+    if out is not None:
+        torch.mm(dy.t(), x, out_dtype=torch.float32, out=out)
+        return out
+    try:
+        return torch.mm(dy.t(), x, out_dtype=torch.float32)
+    except (TypeError, RuntimeError):
+        return torch.mm(dy.t(), x).float()

@@ -216,6 +216,120 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
   return {dx, dw};
 }
 
+// ------------------------------------------------------------------------------------------
+// bf16 MFMA GEMM: C = op(a) @ op(b), op = transpose if trans_*; (trans_a, trans_b) in
+// {(F,T): X·Wᵀ, (F,F): dY·W, (T,F): dYᵀ·X}. Tile/split auto-chosen unless given (bm, bn, splits > 0).
+// ------------------------------------------------------------------------------------------
+struct TileChoice {
+  int bm = 0, bn = 0, splits = 1;
+};
+
+TileChoice choose_tile(int64_t M, int64_t N, int64_t K, bool fp32_out) {
+  static const int cand[][2] = {{256, 160}, {160, 256}, {192, 160}, {160, 160}};
+  TileChoice best;
+  double best_score = -1.0;
+  const int64_t kt = K / 64;
+  for (const auto& c : cand) {
+    if (M % c[0] || N % c[1]) continue;
+    const int64_t tiles = (M / c[0]) * (N / c[1]);
+    const double intensity = (double)c[0] * c[1] / (c[0] + c[1]) / (256.0 * 160.0 / 416.0);
+    for (int s : {1, 2, 3, 4, 5, 6, 8}) {
+      if (s > 1 && (!fp32_out || kt / s < 16)) break;
+      const int64_t wg = tiles * s;
+      const double util = (double)wg / (double)(((wg + 255) / 256) * 256);
+      const double score = util * intensity * (s > 1 ? 0.93 : 1.0);
+      if (score > best_score + 1e-9) {
+        best_score = score;
+        best = {c[0], c[1], s};
+      }
+    }
+  }
+  return best;
+}
+
+bool gemm_supported(const at::Tensor& a, const at::Tensor& b, bool trans_a, bool trans_b) {
+  if (!a.is_cuda() || !b.is_cuda() || a.dim() != 2 || b.dim() != 2) return false;
+  if (a.scalar_type() != at::kBFloat16 || b.scalar_type() != at::kBFloat16) return false;
+  if (trans_a && trans_b) return false;
+  if (a.stride(1) != 1 || b.stride(1) != 1 || a.stride(0) % 8 || b.stride(0) % 8) return false;
+  if (reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 || reinterpret_cast<uintptr_t>(b.data_ptr()) % 16) return false;
+  const int64_t M = trans_a ? a.size(1) : a.size(0), K = trans_a ? a.size(0) : a.size(1);
+  const int64_t N = trans_b ? b.size(0) : b.size(1), Kb = trans_b ? b.size(1) : b.size(0);
+  if (K != Kb || K % 64 || K == 0) return false;
+  if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return false;
+  return choose_tile(M, N, K, true).bm != 0;
+}
+
+at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, bool trans_a, bool trans_b, std::optional<at::ScalarType> out_dtype,
+                const std::optional<at::Tensor>& out, bool accumulate, int64_t bm, int64_t bn, int64_t splits) {
+  TORCH_CHECK(gemm_supported(a, b, trans_a, trans_b), "cs336: gemm shape/layout/dtype not supported (see gemm_supported)");
+  const int64_t M = trans_a ? a.size(1) : a.size(0), K = trans_a ? a.size(0) : a.size(1);
+  const int64_t N = trans_b ? b.size(0) : b.size(1);
+  c10::DeviceGuard g(a.device());
+  at::Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    TORCH_CHECK(c.dim() == 2 && c.size(0) == M && c.size(1) == N && c.stride(1) == 1, "cs336: gemm out must be (M, N) with unit column stride");
+    TORCH_CHECK(c.scalar_type() == at::kFloat || (c.scalar_type() == at::kBFloat16 && !accumulate), "cs336: gemm out dtype");
+  } else {
+    TORCH_CHECK(!accumulate, "cs336: gemm accumulate needs out");
+    c = at::empty({M, N}, a.options().dtype(out_dtype.value_or(at::kBFloat16)));
+  }
+  const bool f32 = c.scalar_type() == at::kFloat;
+  TileChoice t = choose_tile(M, N, K, f32);
+  if (bm > 0 && bn > 0) {
+    TORCH_CHECK(cs336::gemm::tile_supported((int)bm, (int)bn) && M % bm == 0 && N % bn == 0, "cs336: gemm tile");
+    t.bm = (int)bm;
+    t.bn = (int)bn;
+    t.splits = 1;
+  }
+  if (splits > 0) t.splits = f32 ? (int)splits : 1;
+  // the split-K reduction stores float4: needs a 16-B aligned output with ld % 4 == 0
+  if (t.splits > 1 && (reinterpret_cast<uintptr_t>(c.data_ptr()) % 16 || c.stride(0) % 4 || N % 4)) t.splits = 1;
+  cs336::GemmArgs p;
+  p.a = reinterpret_cast<const cs336::bf16_t*>(a.data_ptr());
+  p.b = reinterpret_cast<const cs336::bf16_t*>(b.data_ptr());
+  p.lda = a.stride(0);
+  p.ldb = b.stride(0);
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  if (t.splits > 1) {
+    at::Tensor slabs = at::empty({t.splits, M, N}, a.options().dtype(at::kFloat));
+    p.c = slabs.data_ptr();
+    p.ldc = N;
+    p.split_stride = M * N;
+    TORCH_CHECK(cs336::gemm::gemm_bf16(p, t.bm, t.bn, !trans_a, trans_b, 1, t.splits, stream()), "cs336: gemm launch");
+    cs336::gemm::splitk_reduce(slabs.data_ptr<float>(), c.data_ptr<float>(), M, N, t.splits, c.stride(0), accumulate, stream());
+  } else {
+    p.c = c.data_ptr();
+    p.ldc = c.stride(0);
+    p.split_stride = 0;
+    const int mode = f32 ? (accumulate ? 2 : 1) : 0;
+    TORCH_CHECK(cs336::gemm::gemm_bf16(p, t.bm, t.bn, !trans_a, trans_b, mode, 1, stream()), "cs336: gemm launch");
+  }
+  return c;
+}
+
+at::Tensor gemm_new(const at::Tensor& a, const at::Tensor& b, bool trans_a, bool trans_b, at::ScalarType out_dtype,
+                    int64_t bm, int64_t bn, int64_t splits) {
+  return gemm(a, b, trans_a, trans_b, out_dtype, std::nullopt, false, bm, bn, splits);
+}
+
+void gemm_out(const at::Tensor& a, const at::Tensor& b, bool trans_a, bool trans_b, const at::Tensor& out,
+              bool accumulate, int64_t bm, int64_t bn, int64_t splits) {
+  gemm(a, b, trans_a, trans_b, std::nullopt, out, accumulate, bm, bn, splits);
+}
+
+bool gemm_ok(const at::Tensor& a, const at::Tensor& b, bool trans_a, bool trans_b) {
+  return gemm_supported(a, b, trans_a, trans_b);
+}
+
+std::vector<int64_t> gemm_plan(int64_t M, int64_t N, int64_t K, bool fp32_out) {
+  const TileChoice t = choose_tile(M, N, K, fp32_out);
+  return {t.bm, t.bn, t.splits};
+}
+
 static bool f32_or_bf16(const at::Tensor& t) {
   return t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16;
 }
@@ -493,6 +607,10 @@ TORCH_LIBRARY(cs336, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
   m.def("add_rmsnorm_fwd(Tensor x, Tensor r, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor, Tensor)");
+  m.def("gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, ScalarType out_dtype, int bm=0, int bn=0, int splits=0) -> Tensor");
+  m.def("gemm_out(Tensor a, Tensor b, bool trans_a, bool trans_b, Tensor(a!) out, bool accumulate=False, int bm=0, int bn=0, int splits=0) -> ()");
+  m.def("gemm_ok(Tensor a, Tensor b, bool trans_a, bool trans_b) -> bool", &gemm_ok);
+  m.def("gemm_plan(int M, int N, int K, bool fp32_out) -> int[]", &gemm_plan);
   m.def("rmsnorm_bwd_add(Tensor dy, Tensor x, Tensor weight, Tensor rstd, Tensor dres, bool emit_bf16) -> (Tensor, Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, Tensor? pos, bool inverse) -> Tensor");
   m.def(
@@ -518,6 +636,8 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("fa_bwd", &fa_bwd);
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+  m.impl("gemm", &gemm_new);
+  m.impl("gemm_out", &gemm_out);
   m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
   m.impl("rmsnorm_bwd_add", &rmsnorm_bwd_add);
   m.impl("rope", &rope);

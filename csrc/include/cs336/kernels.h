@@ -24,6 +24,25 @@ void rmsnorm_bwd_add(const void* dy, DType dyt, const void* x, DType xt, const f
                      const void* dres, void* dx, void* dx_bf16, float* dw, float* workspace, int64_t M, int64_t H,
                      hipStream_t s);
 
+// ---- bf16 MFMA GEMM (csrc/gemm/gemm.hip) ----
+// C[M][N] = Σ_k A(m,k) B(k,n); A(m,k) = a[m·lda+k] (K-major) or a[k·lda+m]; B(k,n) = b[n·ldb+k]
+// (K-major) or b[k·ldb+n]. out_mode 0: bf16 C, 1: fp32 C, 2: fp32 C += . splits > 1: fp32 slabs
+// at c + s·split_stride (out_mode 1), summed by splitk_reduce.
+struct GemmArgs {
+  const bf16_t* a;
+  const bf16_t* b;
+  void* c;
+  int64_t lda, ldb, ldc, split_stride;
+  int M, N, K;
+};
+namespace gemm {
+bool tile_supported(int bm, int bn);
+bool gemm_bf16(const GemmArgs& p, int bm, int bn, bool a_kmajor, bool b_kmajor, int out_mode, int splits,
+               hipStream_t s);
+void splitk_reduce(const float* slabs, float* out, int64_t M, int64_t N, int nsplit, int64_t ld_out, bool accumulate,
+                   hipStream_t s);
+}  // namespace gemm
+
 // ---- RoPE (csrc/ops/rope.hip) ----
 // x: (B,H,N,D) strided (elements), out: contiguous (B,N,H,D); cos/sin: (ctx, D/2) fp32;
 // pos: (B,N) int64 or nullptr (position = n).
