@@ -108,7 +108,10 @@ def main(argv=None):
 
     ops.set_backend(args.backend)
     if world > 1:
-        rank, world, device = setup_distributed(backend="nccl")
+        # CS336_DIST_BACKEND=gloo: rehearse the multi-rank path with several ranks on one GPU
+        rank, world, device = setup_distributed(
+            backend=os.environ.get("CS336_DIST_BACKEND", "nccl"), use_gpu=torch.cuda.is_available()
+        )
     else:
         device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
         if device.type == "cuda":

@@ -42,6 +42,7 @@ def setup_distributed(
     master_addr: str | None = None,
     master_port: int | str | None = None,
     timeout_s: float = 600.0,
+    use_gpu: bool | None = None,
 ) -> tuple[int, int, torch.device]:
     """Initialise the default process group; returns ``(rank, world_size, device)``.
 
@@ -57,7 +58,10 @@ def setup_distributed(
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if backend is None:
         backend = default_backend()
-    if backend == "nccl" and torch.cuda.is_available():
+    if use_gpu is None:
+        use_gpu = backend == "nccl"
+    if use_gpu and torch.cuda.is_available():
+        # (gloo + GPU tensors: a multi-rank rehearsal with several ranks sharing one GPU)
         dev = torch.device("cuda", local_rank % torch.cuda.device_count())
         torch.cuda.set_device(dev)
     else:
