@@ -55,6 +55,8 @@ __device__ __forceinline__ int kswz(int r) { return (r >> 1) & 7; }
 // MN-major image: row r = k (S = 2·R bytes, R/16 slots of 32 B); physical slot = logical ^ mswz(r).
 // A tr-read 32-lane group touches rows {0..3, 8..11} (+4 for the second read) of a k32 block,
 // 32 B each: the XOR spreads those 8 rows over the 8 32-B bank slots of a 256-B bank row.
+// (Measured: leaving 160-wide images unswizzled — a 2-way conflict between rows r and r+8 — in
+// exchange for cheaper addressing was slower.)
 template <int S>
 __device__ __forceinline__ int mswz(int r) {
   if constexpr (S % 256 == 0) return (r & 3) | (((r >> 3) & 1) << 2);
@@ -76,7 +78,8 @@ struct Stager {
   static constexpr int kRemW = (kChunks % NT) / 64;
   static constexpr int kPer = kFull + (kRemW ? 1 : 0);
   static_assert(kChunks % 64 == 0, "chunks must fill whole waves");
-  int off[kPer];  // element offset from the tile origin (row0 / col0 at k-tile 0)
+  uint32_t off[kPer];           // BYTE offset from the tile origin (row0 / col0 at k-tile 0)
+  __amdgpu_buffer_rsrc_t rsrc;  // buffer descriptor based at the tile origin (wave-uniform)
   __device__ __forceinline__ static bool has_extra(int wave) {
     return kRemW && (HIGH ? wave >= NT / 64 - kRemW : wave < kRemW);
   }
@@ -86,33 +89,35 @@ struct Stager {
     const int w = HIGH ? wave - (NT / 64 - kRemW) : wave;
     return kFull * NT + w * 64 + lane;
   }
-  __device__ __forceinline__ void init(int wave, int lane, int64_t ld) {
+  __device__ __forceinline__ void init(const bf16_t* origin, int wave, int lane, int64_t ld) {
+    // buffer_load ... lds: 32-bit per-lane VGPR offset + per-k-tile SGPR offset, no 64-bit address
+    // math per load (the host guarantees every operand spans < 2 GiB)
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)origin, (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int q = chunk(i, wave, lane);
       if constexpr (KMAJ) {
         const int r = q >> 3, lc = (q & 7) ^ kswz(r);
-        off[i] = (int)(r * ld) + lc * 8;
+        off[i] = 2u * (uint32_t)(r * ld + lc * 8);
       } else {
         constexpr int S = 2 * R;
         const int byte = 16 * q, r = byte / S, cb = byte % S;
         const int ls = (cb >> 5) ^ mswz<S>(r);
-        off[i] = (int)(r * ld) + ls * 16 + ((cb >> 4) & 1) * 8;
+        off[i] = 2u * (uint32_t)(r * ld + ls * 16 + ((cb >> 4) & 1) * 8);
       }
     }
   }
-  __device__ __forceinline__ static void glds(const bf16_t* src, char* dst) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  __device__ __forceinline__ void glds(uint32_t voff, uint32_t soff, char* dst) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)dst, 16, voff, soff, 0, 0);
   }
-  // issue this wave's glds for one k-tile: src = tile origin advanced to the k-tile
-  __device__ __forceinline__ void issue(const bf16_t* src, char* img, int wave) const {
+  // issue this wave's loads for one k-tile; soff = byte offset of the k-tile from the origin
+  __device__ __forceinline__ void issue(uint32_t soff, char* img, int wave) const {
 #pragma unroll
-    for (int i = 0; i < kFull; ++i) glds(src + off[i], img + 16 * (i * NT + wave * 64));
+    for (int i = 0; i < kFull; ++i) glds(off[i], soff, img + 16 * (i * NT + wave * 64));
     if constexpr (kRemW > 0) {
       if (has_extra(wave)) {
         const int w = HIGH ? wave - (NT / 64 - kRemW) : wave;
-        glds(src + off[kFull], img + 16 * (kFull * NT + w * 64));
+        glds(off[kFull], soff, img + 16 * (kFull * NT + w * 64));
       }
     }
   }
@@ -147,7 +152,9 @@ __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory
 // round-to-nearest-even via v_cvt_pk_bf16_f32 (keeps NaN a NaN, unlike the integer trick)
 __device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
-template <int BM, int BN, int WGM, int WGN, bool AK, bool BKM, int OUT>
+// ABL (ablation builds for profiling only): 1 = no global loads after the prologue (MFMA + LDS
+// reads on stale tiles), 2 = no LDS fragment reads after the first k-tile (MFMA + glds).
+template <int BM, int BN, int WGM, int WGN, bool AK, bool BKM, int OUT, int ABL = 0>
 __global__ __launch_bounds__(WGM* WGN * 64, 1) void gemm_kernel(const GemmArgs p) {
   constexpr int NW = WGM * WGN, NT = NW * 64;
   constexpr int WTM = BM / WGM, WTN = BN / WGN, FM = WTM / 16, FN = WTN / 16;
@@ -179,20 +186,18 @@ __global__ __launch_bounds__(WGM* WGN * 64, 1) void gemm_kernel(const GemmArgs p
 
   SAt sa;
   SBt sb;
-  sa.init(wave, lane, p.lda);
-  sb.init(wave, lane, p.ldb);
-  const bf16_t* a0 = p.a + (AK ? (int64_t)m0 * p.lda : (int64_t)m0);
-  const bf16_t* b0 = p.b + (BKM ? (int64_t)n0 * p.ldb : (int64_t)n0);
-  const int64_t a_step = AK ? kBK : (int64_t)kBK * p.lda;  // elements per k-tile
-  const int64_t b_step = BKM ? kBK : (int64_t)kBK * p.ldb;
+  sa.init(p.a + (AK ? (int64_t)m0 * p.lda : (int64_t)m0), wave, lane, p.lda);
+  sb.init(p.b + (BKM ? (int64_t)n0 * p.ldb : (int64_t)n0), wave, lane, p.ldb);
+  const uint32_t a_step = AK ? 2 * kBK : 2u * kBK * (uint32_t)p.lda;  // bytes per k-tile
+  const uint32_t b_step = BKM ? 2 * kBK : 2u * kBK * (uint32_t)p.ldb;
   // this wave's glds per k-tile: 0, 1 or 2 extra beyond the full rounds (wave-uniform)
   const int extra = (SAt::has_extra(wave) ? 1 : 0) + (SBt::has_extra(wave) ? 1 : 0);
   constexpr int LF = SAt::kFull + SBt::kFull;
 
   auto stage = [&](int kt, int slot) {
     char* img = smem + slot * STAGE;
-    sa.issue(a0 + (int64_t)(kt0 + kt) * a_step, img, wave);
-    sb.issue(b0 + (int64_t)(kt0 + kt) * b_step, img + A_BYTES, wave);
+    sa.issue((uint32_t)(kt0 + kt) * a_step, img, wave);
+    sb.issue((uint32_t)(kt0 + kt) * b_step, img + A_BYTES, wave);
   };
   // own loads of the oldest outstanding tile retired, one younger tile may stay in flight
   auto wait_one_in_flight = [&]() {
@@ -208,6 +213,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 1) void gemm_kernel(const GemmArgs p
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto read = [&](int kt, int ks, bf16x8 (&fa)[FM], bf16x8 (&fb)[FN]) {
+    if (ABL == 2 && kt > 0) return;
     const char* ia = smem + (kt % NS) * STAGE;
     const char* ib = ia + A_BYTES;
 #pragma unroll
@@ -218,12 +224,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, 1) void gemm_kernel(const GemmArgs p
       fb[j] = BKM ? frag_k(ib, wn * WTN + 16 * j, ks, lane) : frag_mn<SB>(ib, wn * WTN + 16 * j, ks, lane);
   };
   auto mma = [&](const bf16x8 (&fa)[FM], const bf16x8 (&fb)[FN]) {
-    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
   };
   // the wait that retires tile t (loads of t+1 may stay in flight) + the barrier that publishes it
   auto land = [&](int t) {
@@ -248,15 +252,46 @@ __global__ __launch_bounds__(WGM* WGN * 64, 1) void gemm_kernel(const GemmArgs p
     if (NS - 1 < nkt) stage(NS - 1, NS - 1);
     read(0, 0, fa0, fb0);
   }
-  for (int kt = 0; kt < nkt; ++kt) {
-    read(kt, 1, fa1, fb1);
-    mma(fa0, fb0);
-    if (kt + 1 < nkt) {
-      land(kt + 1);
-      if (kt + NS < nkt) stage(kt + NS, (kt + NS) % NS);
-      read(kt + 1, 0, fa0, fb0);
+  // ds_read instructions per half step (tr-read fragments take two)
+  constexpr int NR = (AK ? 1 : 2) * FM + (BKM ? 1 : 2) * FN;
+  // interleave the next half's fragment reads into this half's MFMA stream: 1 MFMA, 1 read, ...
+  auto interleave = [&]() {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
     }
-    mma(fa1, fb1);
+    __builtin_amdgcn_sched_group_barrier(0x008, FM * FN - NR > 0 ? FM * FN - NR : 0, 0);
+  };
+  // K-major operands only (ds_read_b128 fragments): the next half's reads ride in this half's
+  // MFMA stream. With tr-read (MN-major) fragments the doubled address/fragment registers spill
+  // at the 256-VGPR budget of 2 waves/SIMD, so those variants read-then-multiply per half and
+  // rely on the SIMD's other wave for overlap.
+  constexpr bool PIPE = AK && BKM;
+  for (int kt = 0; kt < nkt; ++kt) {
+    if constexpr (PIPE) {
+      mma(fa0, fb0);
+      read(kt, 1, fa1, fb1);
+      interleave();
+      if (kt + 1 < nkt) {
+        land(kt + 1);
+        if (ABL != 1 && kt + NS < nkt) stage(kt + NS, (kt + NS) % NS);
+        mma(fa1, fb1);
+        read(kt + 1, 0, fa0, fb0);
+        interleave();
+      } else {
+        mma(fa1, fb1);
+      }
+    } else {
+      if (kt > 0) {
+        land(kt);
+        if (ABL != 1 && kt + NS - 1 < nkt) stage(kt + NS - 1, (kt + NS - 1) % NS);
+        read(kt, 0, fa0, fb0);
+      }
+      mma(fa0, fb0);
+      read(kt, 1, fa0, fb0);
+      mma(fa0, fb0);
+    }
   }
 
   // epilogue: lane holds C[4(l>>4)+r][l&15] of each 16x16 block
@@ -341,6 +376,13 @@ bool tile_supported(int bm, int bn) {
 bool gemm_bf16(const GemmArgs& p, int bm, int bn, bool a_kmajor, bool b_kmajor, int out_mode, int splits,
                hipStream_t s) {
   if (!a_kmajor && b_kmajor) return false;  // (MN, K) orientation is not used by the model
+  static const int abl = getenv("CS336_GEMM_ABLATION") ? atoi(getenv("CS336_GEMM_ABLATION")) : 0;
+  if (abl && bm == 256 && bn == 160 && a_kmajor && b_kmajor && out_mode == 0 && splits == 1) {
+    const dim3 grid((unsigned)((p.M / 256) * (p.N / 160))), block(512);
+    if (abl == 1) hipLaunchKernelGGL((gemm_kernel<256, 160, 4, 2, true, true, 0, 1>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((gemm_kernel<256, 160, 4, 2, true, true, 0, 2>), grid, block, 0, s, p);
+    return true;
+  }
   switch (bm * 1000 + bn) {
     case 256160: return launch_tile<256, 160, 4, 2>(p, a_kmajor, b_kmajor, out_mode, splits, s);
     case 160256: return launch_tile<160, 256, 2, 4>(p, a_kmajor, b_kmajor, out_mode, splits, s);
