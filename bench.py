@@ -135,11 +135,12 @@ def main(argv=None):
         ddp_model = model
     amp = args.dtype == "bf16" and device.type == "cuda"
     okw = dict(lr=args.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01)
+    # bf16 compute-weight shadows written by the AdamW kernel (models/fused.py)
+    shadows = amp and not args.no_shadows
     if args.sharded and world > 1:
-        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, **okw)
+        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw)
     else:
-        # bf16 compute-weight shadows written by the AdamW kernel (models/fused.py)
-        opt = ops.FusedAdamW(model.parameters(), bf16_shadows=amp and not args.no_shadows, **okw)
+        opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)
 
     gen = torch.Generator(device=device)
     gen.manual_seed(1000 + rank)

@@ -62,10 +62,12 @@ def train_ddp(rank: int, world: int, args) -> dict | None:
         check_tol = args.check_tol if args.check_tol is not None else 2.0 * args.lr * (args.steps + args.warmup) + 1e-6
     ddp = wrap_ddp(model, args.variant, bucket_size_mb=args.bucket_mb)
     okw = dict(lr=args.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=args.wd)
+    # bf16 weight shadows (models/fused.py) whenever the step runs under bf16 autocast on GPU
+    shadows = (not args.cpu) and args.dtype == "bf16" and dev.type == "cuda"
     if args.sharded:
-        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, **okw)
+        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw)
     else:
-        opt = ops.FusedAdamW(model.parameters(), **okw)
+        opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)
     ref_opt = ops.FusedAdamW(ref.parameters(), **okw) if args.check else None
     mem_init = _mem(dev)
     assert args.batch % world == 0, "global batch must divide by world size"

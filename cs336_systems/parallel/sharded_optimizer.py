@@ -42,6 +42,16 @@ class ShardedOptimizer(torch.optim.Optimizer):
         self.rank_sizes = [0] * self.world_size
         self._local_group_of: dict[int, int] = {}  # global group idx -> local group idx
         self._sync_plan = None
+        params = list(params)
+        self._shadows = bool(kwargs.get("bf16_shadows", False))
+        if self._shadows:
+            # bf16 compute-weight shadows for EVERY replica parameter (grouped weights share one
+            # shadow storage): the local optimizer rewrites its owned shadows in the update kernel,
+            # the all-gathered ones are re-cast in one multi-tensor launch after the sync
+            from ..models.fused import attach_bf16_shadows
+
+            flat = [p for g in params for p in (g["params"] if isinstance(g, dict) else [g])]
+            attach_bf16_shadows(flat)
         super().__init__(params, defaults=dict(kwargs))
 
     # ------------------------------------------------------------------------------------------
@@ -122,7 +132,7 @@ class ShardedOptimizer(torch.optim.Optimizer):
             if mine:
                 torch.cat([p.detach().reshape(-1) for p in mine], out=send[: sizes[self.rank]])
             dist.all_gather_into_tensor(recv, send, group=self.process_group)
-            dst, src = [], []
+            dst, src, received = [], [], []
             for r in range(self.world_size):
                 if r == self.rank or not per_rank[r]:
                     continue
@@ -131,9 +141,15 @@ class ShardedOptimizer(torch.optim.Optimizer):
                     n = p.numel()
                     dst.append(p.data)
                     src.append(recv[off : off + n].view_as(p))
+                    received.append(p)
                     off += n
             if dst:
                 torch._foreach_copy_(dst, src)
+            if self._shadows and received:
+                # .data copies do not bump p._version: re-cast the shadows explicitly
+                from ..models.fused import refresh_bf16_shadows
+
+                refresh_bf16_shadows(received)
 
     # ------------------------------------------------------------------------------------------
     def state_dict(self):

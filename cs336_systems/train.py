@@ -123,7 +123,7 @@ def train(cfg: TrainConfig) -> dict:
     okw = dict(lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.eps, weight_decay=cfg.wd)
     shadows = dev.type == "cuda" and cfg.dtype == "bf16"
     if cfg.sharded:
-        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, **okw)
+        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw)
     else:
         opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)
 
