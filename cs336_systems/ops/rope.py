@@ -56,9 +56,22 @@ def _normalize_pos(pos: torch.Tensor | None, B: int, N: int) -> torch.Tensor | N
     return p.expand(B, N).to(torch.int64).contiguous()
 
 
+def _hip_layout_ok(x: torch.Tensor) -> bool:
+    """The kernel moves 16 B per access: contiguous last dim, power-of-two head dim in [8, 256],
+    16-byte aligned base and strides (the fused-QKV slices and fresh tensors always are)."""
+    D, es = x.shape[-1], x.element_size()
+    return (
+        x.stride(-1) == 1
+        and 8 <= D <= 256
+        and D & (D - 1) == 0
+        and x.data_ptr() % 16 == 0
+        and all((x.stride(i) * es) % 16 == 0 for i in range(3))
+    )
+
+
 def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor | None = None) -> torch.Tensor:
     """Apply RoPE to ``x`` of shape (..., seq, d)."""
-    if x.dim() == 4 and use_hip(x) and x.stride(-1) == 1:
+    if x.dim() == 4 and use_hip(x) and _hip_layout_ok(x):
         B, H, N, D = x.shape
         p = _normalize_pos(pos, B, N)
         if not isinstance(p, str):

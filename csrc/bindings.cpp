@@ -404,7 +404,15 @@ void rope_into(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin
   TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "cs336: rope x must be (B,H,N,D) with contiguous D");
   TORCH_CHECK(out.dim() == 4 && out.stride(3) == 1 && out.sizes() == x.sizes() && out.dtype() == x.dtype(),
               "cs336: rope out must match x with contiguous D");
-  TORCH_CHECK(x.size(3) % 4 == 0, "cs336: rope head dim must be a multiple of 4");
+  const int64_t D = x.size(3);
+  TORCH_CHECK(D >= 8 && D <= 256 && (D & (D - 1)) == 0, "cs336: rope head dim must be a power of two in [8, 256]");
+  // 16-B vector accesses: every stride and base 16-B aligned
+  const int64_t es = x.element_size();
+  for (const at::Tensor* t : {&x, &out}) {
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0 && (t->stride(0) * es) % 16 == 0 &&
+                    (t->stride(1) * es) % 16 == 0 && (t->stride(2) * es) % 16 == 0,
+                "cs336: rope tensors must be 16-byte aligned with 16-byte aligned strides");
+  }
   TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.is_contiguous() && sin.is_contiguous(), "cs336: rope cache");
   TORCH_CHECK(cos.size(1) * 2 == x.size(3), "cs336: rope cache width");
   c10::DeviceGuard g(x.device());

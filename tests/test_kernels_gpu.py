@@ -44,9 +44,13 @@ def test_rmsnorm(H, xdt, odt):
 # ---------------------------------------------------------------------------------- RoPE
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("with_pos", [False, True])
-def test_rope(dt, with_pos):
+@pytest.mark.parametrize("D", [32, 64, 128])
+def test_rope(dt, with_pos, D):
     torch.manual_seed(0)
-    B, N, H, D, ctx = 2, 33, 3, 64, 64
+    B, N, H, ctx = 2, 33, 3, 64
+    from cs336_systems.ops.rope import _hip_layout_ok
+
+    assert _hip_layout_ok(torch.empty(B, N, H, D, device=DEV, dtype=dt).transpose(1, 2))
     from cs336_systems.models import RotaryEmbedding
 
     re = RotaryEmbedding(ctx, D, 10000.0).to(DEV)
