@@ -22,6 +22,8 @@ Three ideas, all invisible to the state dict (parameter names/shapes are the ref
 
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -145,6 +147,51 @@ def compute_weight(params: list[nn.Parameter], dtype: torch.dtype) -> torch.Tens
 
 
 # ------------------------------------------------------------------------------------------
+# weight-gradient side stream
+# ------------------------------------------------------------------------------------------
+# dW = dYᵀX is off backward's critical path (nothing in backward consumes it), so it runs on a
+# second HIP stream while the main stream continues with dX and the memory-bound kernels of the
+# next layers (RMSNorm/SwiGLU/RoPE backward, FA backward). The main stream waits for the side
+# stream only where a weight gradient is consumed: before a DDP bucket / per-parameter all-reduce
+# (sync_dw_stream) and at the end of the backward pass (an engine callback).
+_SIDE_STREAMS: dict[int, torch.cuda.Stream] = {}
+_state = {"dirty": False, "callback": False}
+
+
+def dw_stream_enabled() -> bool:
+    return os.environ.get("CS336_DW_STREAM", "1") != "0"
+
+
+def _side_stream(device: torch.device) -> torch.cuda.Stream:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _SIDE_STREAMS.get(idx)
+    if s is None:
+        s = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+def sync_dw_stream() -> None:
+    """Make the current stream wait for every weight-gradient GEMM issued so far."""
+    if not _state["dirty"]:
+        return
+    _state["dirty"] = False
+    for idx, s in _SIDE_STREAMS.items():
+        torch.cuda.current_stream(idx).wait_stream(s)
+
+
+def _end_of_backward() -> None:
+    _state["callback"] = False
+    sync_dw_stream()
+
+
+def _mark_side_work() -> None:
+    _state["dirty"] = True
+    if not _state["callback"]:
+        _state["callback"] = True
+        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+
+
+# ------------------------------------------------------------------------------------------
 # fused linear
 # ------------------------------------------------------------------------------------------
 def _mm_fp32_out(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -201,7 +248,28 @@ class FusedLinearFn(torch.autograd.Function):
                 dx = dx.to(ctx.x_dtype)
         if any(ctx.needs_input_grad[1:]):
             target = FusedLinearFn._grad_target(ctx.weights) if dy2.dtype == torch.bfloat16 else None
-            if target is not None:
+            # side stream only when the grads are unset: AccumulateGrad then adopts dW without a
+            # kernel (an accumulate-add on the main stream would race the side-stream GEMM)
+            side = (
+                dy2.is_cuda
+                and dy2.dtype == torch.bfloat16
+                and not torch.is_grad_enabled()
+                and dw_stream_enabled()
+                and all(p.grad is None for p in ctx.weights)
+                and all(dt == torch.float32 for dt in ctx.wdtype)
+            )
+            if side:
+                main = torch.cuda.current_stream(dy2.device)
+                s = _side_stream(dy2.device)
+                s.wait_stream(main)
+                with torch.cuda.stream(s):
+                    dw = gemm.mm_tn_fp32(dy2, x2, out=target) if target is not None else gemm.mm_tn_fp32(dy2, x2)
+                dy2.record_stream(s)
+                x2.record_stream(s)
+                if target is None:
+                    dw.record_stream(main)
+                _mark_side_work()
+            elif target is not None:
                 dw = gemm.mm_tn_fp32(dy2, x2, out=target)
             elif dy2.dtype == torch.bfloat16 and dy2.is_cuda:
                 dw = gemm.mm_tn_fp32(dy2, x2)

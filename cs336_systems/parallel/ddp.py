@@ -36,6 +36,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..models.fused import sync_dw_stream
 from ..utils.profiling import annotate
 from .comm import broadcast_module_, supports_avg
 
@@ -61,6 +62,8 @@ class _DDPBase(nn.Module):
         return self.module(*inputs, **kwargs)
 
     def _all_reduce(self, t: torch.Tensor, async_op: bool):
+        # weight gradients may still be in flight on the dW side stream (models/fused.py)
+        sync_dw_stream()
         op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
         return dist.all_reduce(t, op=op, group=self.process_group, async_op=async_op)
 
