@@ -184,6 +184,14 @@ def _end_of_backward() -> None:
     sync_dw_stream()
 
 
+def _save_transposed(k_in: int, n_out: int) -> bool:
+    """Save Xᵀ for the weight gradient when N_out / K_in >= CS336_XT_RATIO (default 4; 0 = off).
+    Measured per XL projection: W1|W3 (ratio 8) gains 0.19 ms/layer; QKV (3) and O (1) gain less
+    than the transpose costs; W2 (0.25) loses."""
+    r = float(os.environ.get("CS336_XT_RATIO", "4"))
+    return r > 0 and n_out >= r * k_in
+
+
 def _mark_side_work() -> None:
     _state["dirty"] = True
     if not _state["callback"]:
@@ -217,7 +225,11 @@ class FusedLinearFn(torch.autograd.Function):
         if x2.dtype != cdt:
             x2 = x2.to(cdt)
         y = gemm.mm_nt(x2, w)
-        ctx.save_for_backward(x2, w)
+        # For wide projections (N_out >= r * K_in, e.g. W1|W3: 12800 vs 1600) save Xᵀ instead of X:
+        # the weight-gradient GEMM dYᵀX then reads both operands token-contiguous, which hipBLASLt
+        # runs 1.4x faster on MI355X (profiles/r1_gemm_dw_layouts.json), for one small transpose
+        ctx.xt = x2.is_cuda and any(ctx.needs_input_grad[1:]) and _save_transposed(x2.shape[1], w.shape[0])
+        ctx.save_for_backward(x2.t().contiguous() if ctx.xt else x2, w)
         ctx.x_shape = x.shape
         ctx.x_dtype = x.dtype
         ctx.rows = [p.shape[0] for p in weights]
@@ -258,23 +270,25 @@ class FusedLinearFn(torch.autograd.Function):
                 and all(p.grad is None for p in ctx.weights)
                 and all(dt == torch.float32 for dt in ctx.wdtype)
             )
+            if ctx.xt:  # x2 holds Xᵀ (K_in, tokens)
+                dw_fn = lambda out=None: gemm.mm_tn_fp32_xt(dy2, x2, out=out)  # noqa: E731
+            else:
+                dw_fn = lambda out=None: gemm.mm_tn_fp32(dy2, x2, out=out)  # noqa: E731
             if side:
                 main = torch.cuda.current_stream(dy2.device)
                 s = _side_stream(dy2.device)
                 s.wait_stream(main)
                 with torch.cuda.stream(s):
-                    dw = gemm.mm_tn_fp32(dy2, x2, out=target) if target is not None else gemm.mm_tn_fp32(dy2, x2)
+                    dw = dw_fn(target)
                 dy2.record_stream(s)
                 x2.record_stream(s)
                 if target is None:
                     dw.record_stream(main)
                 _mark_side_work()
-            elif target is not None:
-                dw = gemm.mm_tn_fp32(dy2, x2, out=target)
-            elif dy2.dtype == torch.bfloat16 and dy2.is_cuda:
-                dw = gemm.mm_tn_fp32(dy2, x2)
+            elif target is not None or (dy2.dtype == torch.bfloat16 and dy2.is_cuda):
+                dw = dw_fn(target)
             else:
-                dw = _mm_fp32_out(dy2.t(), x2)
+                dw = _mm_fp32_out(dy2.t(), x2.t() if ctx.xt else x2)
             dw_parts = list(torch.split(dw, ctx.rows, 0))
             dw_parts = [g if g.dtype == dt else g.to(dt) for g, dt in zip(dw_parts, ctx.wdtype)]
         return (dx, *(dw_parts if dw_parts is not None else [None] * len(ctx.rows)))

@@ -39,6 +39,15 @@ def mm_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return torch.mm(dy, w)
 
 
+def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``dy.T @ xt.T`` with an fp32 result: the weight gradient from a token-contiguous ``Xᵀ``
+    (K_in, tokens). hipBLASLt only: its NT kernels are the fast ones for this layout."""
+    if out is not None:
+        torch.mm(dy.t(), xt.t(), out_dtype=torch.float32, out=out)
+        return out
+    return torch.mm(dy.t(), xt.t(), out_dtype=torch.float32)
+
+
 def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """``dy.T @ x`` with an fp32 result (weight gradient), written into ``out`` when given."""
     if hip_gemm_enabled() and _ok(dy, x, True, False):

@@ -30,11 +30,17 @@ def main():
         w = torch.randn(N, K, device="cuda").bfloat16()
         dy = torch.randn(T, N, device="cuda").bfloat16()
         fl = 2.0 * T * N * K
+        dyT, xT = dy.t().contiguous(), x.t().contiguous()  # token-contiguous copies
         cases = {
             # name: (torch fn, a, b, trans_a, trans_b, out dtype)
             "fwd": (lambda: x @ w.t(), x, w, False, True, torch.bfloat16),
             "dx": (lambda: dy @ w, dy, w, False, False, torch.bfloat16),
             "dw": (lambda: torch.mm(dy.t(), x, out_dtype=torch.float32), dy, x, True, False, torch.float32),
+            # the same weight gradient from token-contiguous (K-major) operands
+            "dw_kk": (lambda: torch.mm(dyT, xT.t(), out_dtype=torch.float32), dyT, xT, False, True, torch.float32),
+            # mixed: only X token-contiguous (saved transposed from the forward) / only dY
+            "dw_xt": (lambda: torch.mm(dy.t(), xT.t(), out_dtype=torch.float32), dy, xT, True, True, torch.float32),
+            "dw_dyt": (lambda: torch.mm(dyT, x, out_dtype=torch.float32), dyT, x, False, False, torch.float32),
         }
         for case, (tfn, a, b, ta, tb, odt) in cases.items():
             M_, N_ = (a.shape[1] if ta else a.shape[0]), (b.shape[0] if tb else b.shape[1])
