@@ -33,6 +33,18 @@ def _rms_bwd(dy, x, w, rstd):
     return torch.empty_like(x), w.new_empty(w.shape, dtype=torch.float32)
 
 
+@register_fake("cs336::transpose2d")
+def _transpose2d(x):
+    return x.new_empty((x.shape[1], x.shape[0]))
+
+
+@register_fake("cs336::gemm")
+def _gemm(a, b, trans_a, trans_b, out_dtype, bm=0, bn=0, splits=0):
+    M = a.shape[1] if trans_a else a.shape[0]
+    N = b.shape[0] if trans_b else b.shape[1]
+    return a.new_empty((M, N), dtype=out_dtype)
+
+
 @register_fake("cs336::add_rmsnorm_fwd")
 def _add_rms_fwd(x, r, w, eps, out_dtype):
     return torch.empty_like(x), x.new_empty(x.shape, dtype=out_dtype or x.dtype), x.new_empty((x.shape[0],), dtype=torch.float32)

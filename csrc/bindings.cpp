@@ -330,6 +330,20 @@ std::vector<int64_t> gemm_plan(int64_t M, int64_t N, int64_t K, bool fp32_out) {
   return {t.bm, t.bn, t.splits};
 }
 
+// out = x.t().contiguous() for a 2-D 16-bit tensor with unit column stride
+at::Tensor transpose2d(const at::Tensor& x) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.element_size() == 2, "cs336: transpose2d needs a 2-D 16-bit row-major tensor");
+  TORCH_CHECK(x.size(0) % 8 == 0 && x.size(1) % 8 == 0 && x.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "cs336: transpose2d needs dims and row stride multiples of 8 and a 16-B aligned base");
+  c10::DeviceGuard g(x.device());
+  at::Tensor out = at::empty({x.size(1), x.size(0)}, x.options());
+  if (x.numel() == 0) return out;
+  cs336::transpose16(x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0), (int)x.size(0), (int)x.size(1), stream());
+  return out;
+}
+
 static bool f32_or_bf16(const at::Tensor& t) {
   return t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16;
 }
@@ -615,6 +629,7 @@ TORCH_LIBRARY(cs336, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
   m.def("add_rmsnorm_fwd(Tensor x, Tensor r, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor, Tensor)");
+  m.def("transpose2d(Tensor x) -> Tensor");
   m.def("gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, ScalarType out_dtype, int bm=0, int bn=0, int splits=0) -> Tensor");
   m.def("gemm_out(Tensor a, Tensor b, bool trans_a, bool trans_b, Tensor(a!) out, bool accumulate=False, int bm=0, int bn=0, int splits=0) -> ()");
   m.def("gemm_ok(Tensor a, Tensor b, bool trans_a, bool trans_b) -> bool", &gemm_ok);
@@ -644,6 +659,7 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("fa_bwd", &fa_bwd);
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+  m.impl("transpose2d", &transpose2d);
   m.impl("gemm", &gemm_new);
   m.impl("gemm_out", &gemm_out);
   m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);

@@ -24,6 +24,10 @@ void rmsnorm_bwd_add(const void* dy, DType dyt, const void* x, DType xt, const f
                      const void* dres, void* dx, void* dx_bf16, float* dw, float* workspace, int64_t M, int64_t H,
                      hipStream_t s);
 
+// ---- 2-byte transpose (csrc/ops/transpose.hip): out[c][r] = in[r][c]; R, C multiples of 8,
+// 16-B aligned rows
+void transpose16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int R, int C, hipStream_t s);
+
 // ---- bf16 MFMA GEMM (csrc/gemm/gemm.hip) ----
 // C[M][N] = Σ_k A(m,k) B(k,n); A(m,k) = a[m·lda+k] (K-major) or a[k·lda+m]; B(k,n) = b[n·ldb+k]
 // (K-major) or b[k·ldb+n]. out_mode 0: bf16 C, 1: fp32 C, 2: fp32 C += . splits > 1: fp32 slabs

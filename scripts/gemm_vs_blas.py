@@ -31,10 +31,13 @@ def main():
         dy = torch.randn(T, N, device="cuda").bfloat16()
         fl = 2.0 * T * N * K
         dyT, xT = dy.t().contiguous(), x.t().contiguous()  # token-contiguous copies
+        wT = w.t().contiguous()
         cases = {
             # name: (torch fn, a, b, trans_a, trans_b, out dtype)
             "fwd": (lambda: x @ w.t(), x, w, False, True, torch.bfloat16),
             "dx": (lambda: dy @ w, dy, w, False, False, torch.bfloat16),
+            # input gradient from a transposed weight copy Wᵀ (K_in, N_out): both operands K-major
+            "dx_wt": (lambda: dy @ wT.t(), dy, wT, False, True, torch.bfloat16),
             "dw": (lambda: torch.mm(dy.t(), x, out_dtype=torch.float32), dy, x, True, False, torch.float32),
             # the same weight gradient from token-contiguous (K-major) operands
             "dw_kk": (lambda: torch.mm(dyT, xT.t(), out_dtype=torch.float32), dyT, xT, False, True, torch.float32),

@@ -313,3 +313,16 @@ def test_bf16_shadows_track_master_weights():
     with torch.no_grad():
         w.add_(1.0)  # out-of-band edit invalidates the shadow -> forward falls back to casting
     assert not shadow_valid(w)
+
+
+# ---------------------------------------------------------------------------------- transpose
+@pytest.mark.parametrize("shape", [(64, 64), (1600, 4800), (120, 72), (8, 200)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_transpose2d(shape, dt):
+    from cs336_systems.ops._ext import ops as _hip
+
+    x = torch.randn(*shape, device=DEV).to(dt)
+    torch.testing.assert_close(_hip().transpose2d(x), x.t().contiguous(), rtol=0, atol=0)
+    big = torch.randn(shape[0], shape[1] + 16, device=DEV).to(dt)
+    v = big[:, 8 : 8 + shape[1]]  # strided rows
+    torch.testing.assert_close(_hip().transpose2d(v), v.t().contiguous(), rtol=0, atol=0)
