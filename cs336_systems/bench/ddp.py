@@ -49,8 +49,8 @@ def _peak(dev):
 
 
 def train_ddp(rank: int, world: int, args) -> dict | None:
-    backend = "gloo" if args.cpu else None
-    rank, world, dev = setup_distributed(rank, world, backend=backend)
+    backend = "gloo" if (args.cpu or args.gloo_gpu) else None
+    rank, world, dev = setup_distributed(rank, world, backend=backend, use_gpu=True if args.gloo_gpu else None)
     torch.manual_seed(args.seed)
     model = build_model(args.size, args.ctx, device=dev)
     if args.check:
@@ -181,6 +181,7 @@ def parse(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--gloo-gpu", action="store_true", help="gloo over GPU tensors: several ranks may share one GPU")
     ap.add_argument("--world-size", type=int, default=2)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--check-tol", type=float, default=None)
