@@ -179,6 +179,13 @@ def sync_dw_stream() -> None:
         torch.cuda.current_stream(idx).wait_stream(s)
 
 
+def dw_stream_for(t: torch.Tensor) -> torch.cuda.Stream | None:
+    """The side stream of ``t``'s device if weight-gradient work is pending on it, else None."""
+    if not (_state["dirty"] and t.is_cuda):
+        return None
+    return _SIDE_STREAMS.get(t.device.index if t.device.index is not None else torch.cuda.current_device())
+
+
 def _end_of_backward() -> None:
     _state["callback"] = False
     sync_dw_stream()

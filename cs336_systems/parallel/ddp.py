@@ -36,7 +36,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ..models.fused import sync_dw_stream
+from ..models.fused import dw_stream_for, sync_dw_stream
 from ..utils.profiling import annotate
 from .comm import broadcast_module_, supports_avg
 
@@ -62,10 +62,17 @@ class _DDPBase(nn.Module):
         return self.module(*inputs, **kwargs)
 
     def _all_reduce(self, t: torch.Tensor, async_op: bool):
-        # weight gradients may still be in flight on the dW side stream (models/fused.py)
-        sync_dw_stream()
         op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
-        return dist.all_reduce(t, op=op, group=self.process_group, async_op=async_op)
+        # Weight gradients may still be in flight on the dW side stream (models/fused.py). Issue
+        # the collective from that stream after it has caught up with the main stream: the
+        # communication stream then waits for both, and the main stream keeps running backward.
+        side = dw_stream_for(t)
+        if side is None or not async_op:
+            sync_dw_stream()
+            return dist.all_reduce(t, op=op, group=self.process_group, async_op=async_op)
+        side.wait_stream(torch.cuda.current_stream(t.device))
+        with torch.cuda.stream(side):
+            return dist.all_reduce(t, op=op, group=self.process_group, async_op=True)
 
     def _finish_mean(self, t: torch.Tensor) -> None:
         if not self._avg and self.world_size > 1:
