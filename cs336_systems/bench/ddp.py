@@ -68,6 +68,9 @@ def train_ddp(rank: int, world: int, args) -> dict | None:
         opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw)
     else:
         opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)
+        if args.overlap_opt and args.clip == 0:
+            # AdamW per reduced bucket during backward (needs an AVG backend: RCCL)
+            opt.enable_backward_overlap(ddp=ddp if args.variant == "bucketed" else None)
     ref_opt = ops.FusedAdamW(ref.parameters(), **okw) if args.check else None
     mem_init = _mem(dev)
     assert args.batch % world == 0, "global batch must divide by world size"
@@ -170,6 +173,7 @@ def parse(argv=None):
     ap.add_argument("--variant", default="bucketed", choices=sorted(DDP_VARIANTS))
     ap.add_argument("--bucket-mb", type=float, default=DEFAULT_BUCKET_MB)
     ap.add_argument("--sharded", action="store_true")
+    ap.add_argument("--overlap-opt", action="store_true", help="AdamW overlapped with backward (bucketed: per reduced bucket)")
     ap.add_argument("--size", default="xl")
     ap.add_argument("--ctx", type=int, default=512)
     ap.add_argument("--batch", type=int, default=16, help="global batch (split over ranks)")

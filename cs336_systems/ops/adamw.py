@@ -11,6 +11,22 @@ for 3.4 B params on H100). Here the whole model is one launch per (
 group: a chunk table (tensor pointer, chunk offset) is built on the host and every workgroup
 streams one 16 KiB-per-wave chunk with 16-byte vector loads, so the step is HBM-bound
 (28 B/param: read p,g,m,v; write p,m,v).
+
+**Optimizer step overlapped with backward** (``overlap_backward=True``, GPU only). A parameter's
+update needs nothing but its own final gradient, and AdamW is HBM-bound while backward is
+MFMA-bound, so the update of the last layers runs on a second HIP stream while backward still
+computes the gradients of the first ones. Parameters are handed over as soon as their gradient is
+final: single process — from ``post_accumulate_grad`` hooks, in chunks of ~256 MB of fp32 params
+(few launches, each long enough to stream at full bandwidth); with
+:class:`~cs336_systems.parallel.DDPBucketed` (``ddp=``) — per bucket, right after its all-reduce is
+issued, the optimizer stream waiting on that collective (``Work.wait()`` on the optimizer stream,
+the host never blocks). Each hand-over also waits for the main stream and the weight-gradient side
+stream (``models/fused.py``); ``step()`` updates what was not handed over and makes the main
+stream wait for the optimizer stream, so the next forward reads updated weights and bf16 shadows.
+Requirements: one backward per step, no gradient transform between backward and ``step()``
+(clipping — the drivers enable the overlap only when ``clip == 0``), the learning rate set before
+backward. The update math is unchanged, so results are bitwise identical to the plain step
+(``tests/test_opt_overlap_gpu.py``).
 """
 
 from __future__ import annotations
@@ -32,6 +48,20 @@ def adamw_ref_(p, g, m, v, lr, beta1, beta2, eps, wd, t):
     p.sub_(lr * wd * p)
 
 
+class _Overlap:
+    """Bookkeeping of the backward-overlapped update (see the module docstring)."""
+
+    def __init__(self, device: torch.device, chunk_numel: int):
+        self.stream = torch.cuda.Stream(device=device)
+        self.chunk_numel = chunk_numel
+        self.pending: list[torch.nn.Parameter] = []
+        self.pending_numel = 0
+        self.stepped: set[int] = set()
+        self.used = False
+        self.active = True
+        self.hooks: list = []
+
+
 class FusedAdamW(torch.optim.Optimizer):
     """Drop-in for ``cs336_basics.optimizer.AdamW`` that runs one HIP launch per step.
 
@@ -47,6 +77,8 @@ class FusedAdamW(torch.optim.Optimizer):
         eps: float = 1e-8,
         weight_decay: float = 0.01,
         bf16_shadows: bool = False,
+        overlap_backward: bool = False,
+        ddp=None,
     ):
         """``bf16_shadows=True``: every 2-D fp32 GPU weight gets a bf16 copy that the update kernel
         rewrites in the same pass; the model's GEMMs read it instead of re-casting under autocast
@@ -64,6 +96,50 @@ class FusedAdamW(torch.optim.Optimizer):
             from ..models.fused import attach_bf16_shadows
 
             attach_bf16_shadows([p for g in self.param_groups for p in g["params"]])
+        self._ov: _Overlap | None = None
+        if overlap_backward:
+            self.enable_backward_overlap(ddp=ddp)
+
+    # ------------------------------------------------------------------------------------------
+    # update launches
+    # ------------------------------------------------------------------------------------------
+    def _update(self, items: list[tuple[dict, torch.nn.Parameter]]) -> None:
+        """Update ``(group, param)`` pairs whose ``.grad`` is set, on the current stream."""
+        from ..models.fused import get_shadow, mark_shadow_synced
+
+        # bucket by (group, device, dtype, t, shadow) so each launch has one set of
+        # hyper-parameters, one bias correction and an all-or-nothing shadow list
+        buckets: dict[tuple, tuple[dict, list, list, list, list, list]] = {}
+        for group, p in items:
+            if p.grad.is_sparse:
+                raise RuntimeError("AdamW does not support sparse gradients")
+            state = self.state[p]
+            if "m" not in state:
+                state["m"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                state["v"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                state["t"] = 1
+            sh = get_shadow(p)
+            key = (id(group), p.device, p.dtype, p.grad.dtype, state["t"], sh is not None)
+            b = buckets.setdefault(key, (group, [], [], [], [], []))
+            b[1].append(p)
+            b[2].append(p.grad)
+            b[3].append(state["m"])
+            b[4].append(state["v"])
+            if sh is not None:
+                b[5].append(sh)
+            state["t"] += 1
+        for key, (group, ps, gs, ms, vs, ss) in buckets.items():
+            t = key[4]
+            lr, (beta1, beta2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+            if use_hip(ps[0]) and all(x.is_contiguous() for x in ps + gs + ms + vs + ss):
+                ops().adamw_step(ps, gs, ms, vs, ss, lr, beta1, beta2, eps, wd, t)
+            else:
+                for p, g, m, v in zip(ps, gs, ms, vs):
+                    adamw_ref_(p, g.to(p.dtype), m, v, lr, beta1, beta2, eps, wd, t)
+                for p, s in zip(ps, ss):
+                    s.copy_(p)
+            for p in ps if ss else ():
+                mark_shadow_synced(p)
 
     @torch.no_grad()
     def step(self, closure: Callable | None = None):
@@ -71,47 +147,92 @@ class FusedAdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for group in self.param_groups:
-            lr = group["lr"]
-            beta1, beta2 = group["betas"]
-            eps = group["eps"]
-            wd = group["weight_decay"]
-            from ..models.fused import get_shadow, mark_shadow_synced
-
-            # bucket by (device, dtype, t, shadow) so each launch has one bias correction and an
-            # all-or-nothing shadow list
-            buckets: dict[tuple, tuple[list, list, list, list, list]] = {}
-            for p in group["params"]:
-                if p.grad is None:
-                    continue
-                if p.grad.is_sparse:
-                    raise RuntimeError("AdamW does not support sparse gradients")
-                state = self.state[p]
-                if "m" not in state:
-                    state["m"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    state["v"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    state["t"] = 1
-                sh = get_shadow(p)
-                key = (p.device, p.dtype, p.grad.dtype, state["t"], sh is not None)
-                b = buckets.setdefault(key, ([], [], [], [], []))
-                b[0].append(p)
-                b[1].append(p.grad)
-                b[2].append(state["m"])
-                b[3].append(state["v"])
-                if sh is not None:
-                    b[4].append(sh)
-                state["t"] += 1
-            for (dev, _, _, t, _), (ps, gs, ms, vs, ss) in buckets.items():
-                if use_hip(ps[0]) and all(x.is_contiguous() for x in ps + gs + ms + vs + ss):
-                    ops().adamw_step(ps, gs, ms, vs, ss, lr, beta1, beta2, eps, wd, t)
-                else:
-                    for p, g, m, v in zip(ps, gs, ms, vs):
-                        adamw_ref_(p, g.to(p.dtype), m, v, lr, beta1, beta2, eps, wd, t)
-                    for p, s in zip(ps, ss):
-                        s.copy_(p)
-                for p in ps if ss else ():
-                    mark_shadow_synced(p)
+        ov = self._ov
+        if ov is not None:
+            self._flush()
+        items = [
+            (g, p)
+            for g in self.param_groups
+            for p in g["params"]
+            if p.grad is not None and (ov is None or id(p) not in ov.stepped)
+        ]
+        if items:
+            self._update(items)
+        if ov is not None:
+            ov.stepped.clear()
+            if ov.used:
+                torch.cuda.current_stream(ov.stream.device).wait_stream(ov.stream)
+                ov.used = False
         return loss
+
+    # ------------------------------------------------------------------------------------------
+    # backward overlap
+    # ------------------------------------------------------------------------------------------
+    def enable_backward_overlap(self, ddp=None, chunk_mb: float = 256.0) -> bool:
+        """Start updating parameters during backward (module docstring). Returns False (and stays
+        off) when it cannot apply: CPU parameters, or a DDP wrapper whose reduced gradients are not
+        final when its collective completes (non-AVG backends divide afterwards)."""
+        params = [p for g in self.param_groups for p in g["params"]]
+        if not params or not all(p.is_cuda for p in params) or self._ov is not None:
+            return self._ov is not None
+        if ddp is not None and not (hasattr(ddp, "add_bucket_callback") and getattr(ddp, "_avg", False)):
+            return False
+        ov = _Overlap(params[0].device, max(1, int(chunk_mb * 2**20 / 4)))
+        self._group_of = {id(p): g for g in self.param_groups for p in g["params"]}
+        if ddp is not None:
+            ddp.add_bucket_callback(self._on_bucket_reduced)
+        else:
+            ov.hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in params if p.requires_grad]
+        self._ov = ov
+        return True
+
+    def set_backward_overlap(self, active: bool) -> None:
+        """Pause (e.g. for gradient-accumulation micro-steps) or resume the overlapped update."""
+        if self._ov is not None:
+            self._ov.active = active
+
+    @property
+    def overlaps_backward(self) -> bool:
+        return self._ov is not None and self._ov.active
+
+    def _on_grad_ready(self, p: torch.nn.Parameter) -> None:
+        ov = self._ov
+        if ov is None or not ov.active or p.grad is None:
+            return
+        ov.pending.append(p)
+        ov.pending_numel += p.numel()
+        if ov.pending_numel >= ov.chunk_numel:
+            self._flush()
+
+    def _on_bucket_reduced(self, params, work) -> None:
+        ov = self._ov
+        if ov is None or not ov.active:
+            return
+        ov.pending.extend(p for p in params if p.grad is not None)
+        self._flush(work)
+
+    @torch.no_grad()
+    def _flush(self, work=None) -> None:
+        ov = self._ov
+        ps = ov.pending
+        if not ps:
+            return
+        ov.pending, ov.pending_numel = [], 0
+        from ..models.fused import dw_stream_for
+
+        s = ov.stream
+        s.wait_stream(torch.cuda.current_stream(s.device))
+        side = dw_stream_for(ps[0].grad)  # weight-gradient GEMMs still in flight
+        if side is not None:
+            s.wait_stream(side)
+        with torch.cuda.stream(s):
+            if work is not None:
+                work.wait()
+            self._update([(self._group_of[id(p)], p) for p in ps])
+        for p in ps:
+            p.grad.record_stream(s)
+            ov.stepped.add(id(p))
+        ov.used = True
 
 
 def multi_tensor_l2norm(tensors: list[torch.Tensor]) -> torch.Tensor:

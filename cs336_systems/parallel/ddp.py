@@ -232,7 +232,14 @@ class DDPBucketed(_DDPBase):
                 # grad is unset (models/fused.py), so _adopt finds it already in place
                 p._cs336_grad_out = self._views[p]
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in params]
+        self._bucket_callbacks = []
         self.zero_grad()
+
+    def add_bucket_callback(self, fn) -> None:
+        """``fn(params, work)`` runs right after a bucket's all-reduce is issued (``work`` is its
+        async handle; with AVG the reduced gradients are final once it completes). Used by
+        :class:`~cs336_systems.ops.FusedAdamW` to update each bucket during backward."""
+        self._bucket_callbacks.append(fn)
 
     # ---- grad buffer management -------------------------------------------------------------
     def zero_grad(self, set_to_none: bool = False) -> None:
@@ -259,6 +266,8 @@ class DDPBucketed(_DDPBase):
         with annotate(f"comm.bucket{b.idx}"):
             b.handle = self._all_reduce(b.flat, async_op=True)
         b.launched = True
+        for fn in self._bucket_callbacks:
+            fn(b.params, b.handle)
 
     def _on_grad_ready(self, p: nn.Parameter) -> None:
         b = self._param_bucket[p]
