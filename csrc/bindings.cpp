@@ -204,6 +204,7 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
                                                const at::Tensor& rstd) {
   check_cuda(dy, "dy");
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "cs336: rmsnorm_bwd shapes");
+  TORCH_CHECK(x.size(1) % 4 == 0, "cs336: rmsnorm_bwd needs a hidden size divisible by 4");
   c10::DeviceGuard g(x.device());
   at::Tensor dx = at::empty_like(x);
   if (x.size(0) == 0) return {dx, at::zeros({x.size(1)}, x.options().dtype(at::kFloat))};
@@ -377,6 +378,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add(const at::Tensor&
                                                                const at::Tensor& dres, bool emit_bf16) {
   check_cuda(dy, "dy");
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "cs336: rmsnorm_bwd_add shapes");
+  TORCH_CHECK(x.size(1) % 4 == 0, "cs336: rmsnorm_bwd_add needs a hidden size divisible by 4");
   TORCH_CHECK(dres.is_contiguous() && dres.sizes() == x.sizes() && dres.scalar_type() == x.scalar_type(),
               "cs336: rmsnorm_bwd_add dres must match x");
   TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == x.size(1),

@@ -100,6 +100,9 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const typename Elem<TD
     const auto* dyr = dy + row * H;
     const float r = rstd[row];
     float4 xv[NV], gv[NV];
+    // ADD: the residual gradient is loaded with x and dy, before the row reduction, so its latency
+    // hides under the reduction instead of stalling the output pass
+    float4 dv[ADD ? NV : 1];
     float dot = 0.f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
@@ -107,12 +110,16 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const typename Elem<TD
       if (i < H4) {
         xv[k] = load4<TX>(xr + 4 * i);
         gv[k] = load4<TDY>(dyr + 4 * i);
-        dot += wv[k].x * gv[k].x * xv[k].x + wv[k].y * gv[k].y * xv[k].y + wv[k].z * gv[k].z * xv[k].z +
-               wv[k].w * gv[k].w * xv[k].w;
+        if constexpr (ADD) dv[k] = load4<TX>(dres + row * H + 4 * i);
       } else {
         xv[k] = gv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (ADD) dv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+      dot += wv[k].x * gv[k].x * xv[k].x + wv[k].y * gv[k].y * xv[k].y + wv[k].z * gv[k].z * xv[k].z +
+             wv[k].w * gv[k].w * xv[k].w;
     dot = wave_sum(dot);
     const float c = r * r * r * invH * dot;
     auto* dxr = dx + row * H;
@@ -126,8 +133,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const typename Elem<TD
         o.z = r * wv[k].z * gv[k].z - c * xv[k].z;
         o.w = r * wv[k].w * gv[k].w - c * xv[k].w;
         if constexpr (ADD) {
-          const float4 d = load4<TX>(dres + row * H + 4 * i);
-          o.x += d.x; o.y += d.y; o.z += d.z; o.w += d.w;
+          o.x += dv[k].x; o.y += dv[k].y; o.z += dv[k].z; o.w += dv[k].w;
           if (dx2) store4<BF16>(dx2 + row * H + 4 * i, o);
         }
         store4<TX>(dxr + 4 * i, o);
@@ -164,17 +170,36 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const typename Elem<TD
   for (int i = threadIdx.x; i < H4; i += 256) reinterpret_cast<float4*>(wr)[i] = reinterpret_cast<float4*>(red)[i];
 }
 
-// out[s][j] = sum over partial rows p in split s of ws[p][j]; grid (col tiles of 256, splits)
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ ws, float* __restrict__ out, int P,
+// out[s][j] = sum over the partial rows p of split s of ws[p][j] (H % 4 == 0). Block = 64 float4
+// columns x 8 row slices; the slices are folded through LDS in a fixed order (deterministic).
+// grid (ceil(H/256), splits)
+__global__ __launch_bounds__(512) void colsum_kernel(const float* __restrict__ ws, float* __restrict__ out, int P,
                                                      int H) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  __shared__ float4 red[8][64];
+  const int H4 = H >> 2;
+  const int c4 = blockIdx.x * 64 + (threadIdx.x & 63), slice = threadIdx.x >> 6;
   const int S = gridDim.y, s = blockIdx.y;
   const int per = (P + S - 1) / S;
   const int p0 = s * per, p1 = min(P, p0 + per);
-  float acc = 0.f;
-  if (j < H)
-    for (int p = p0; p < p1; ++p) acc += ws[(int64_t)p * H + j];
-  if (j < H) out[(int64_t)s * H + j] = acc;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c4 < H4) {
+    const float4* w4 = reinterpret_cast<const float4*>(ws);
+#pragma unroll 4
+    for (int p = p0 + slice; p < p1; p += 8) {
+      const float4 v = w4[(int64_t)p * H4 + c4];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[slice][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (slice == 0 && c4 < H4) {
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      const float4 v = red[k][threadIdx.x];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(out + (int64_t)s * H)[c4] = acc;
+  }
 }
 
 template <int NV, typename F>
@@ -219,13 +244,13 @@ void rmsnorm_fwd(const void* x, DType xt, const void* w, DType wt, void* y, DTyp
   });
 }
 
-// ~2 rows per wave: 4 waves x 2 rows per workgroup keeps ~16 waves/CU streaming (the row loop is
-// latency-bound at low occupancy), capped so the partial-row workspace stays small.
+// ~3 rows per wave: 1024 workgroups of 4 waves = 16 waves/CU (the occupancy the ~130-VGPR row loop
+// allows) in one round for the XL rows (M = 12288), capped so the partial-row workspace stays small.
 static int bwd_blocks(int64_t M) {
-  int64_t nb = (M + 7) / 8;
-  return (int)(nb < 4096 ? (nb > 0 ? nb : 1) : 4096);
+  int64_t nb = (M + 11) / 12;
+  return (int)(nb < 1024 ? (nb > 0 ? nb : 1) : 1024);
 }
-constexpr int kColSplits = 32;
+constexpr int kColSplits = 16;
 
 int rmsnorm_bwd_workspace_rows(int64_t M, int64_t H) {
   (void)H;
@@ -253,9 +278,9 @@ void rmsnorm_bwd(const void* dy, DType dyt, const void* x, DType xt, const void*
     });
   });
   float* split = workspace + (int64_t)nb * H;
-  const unsigned ct = (unsigned)((H + 255) / 256);
-  hipLaunchKernelGGL(colsum_kernel, dim3(ct, kColSplits), dim3(256), 0, s, workspace, split, nb, (int)H);
-  hipLaunchKernelGGL(colsum_kernel, dim3(ct, 1), dim3(256), 0, s, split, dw, kColSplits, (int)H);
+  const unsigned ct = (unsigned)((H / 4 + 63) / 64);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ct, kColSplits), dim3(512), 0, s, workspace, split, nb, (int)H);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ct, 1), dim3(512), 0, s, split, dw, kColSplits, (int)H);
 }
 
 // Fused residual variants: fp32 weights only (master weights), stream/branch dtypes fp32 or bf16.
@@ -304,9 +329,9 @@ void rmsnorm_bwd_add(const void* dy, DType dyt, const void* x, DType xt, const f
     });
   });
   float* split = workspace + (int64_t)nb * H;
-  const unsigned ct = (unsigned)((H + 255) / 256);
-  hipLaunchKernelGGL(colsum_kernel, dim3(ct, kColSplits), dim3(256), 0, s, workspace, split, nb, (int)H);
-  hipLaunchKernelGGL(colsum_kernel, dim3(ct, 1), dim3(256), 0, s, split, dw, kColSplits, (int)H);
+  const unsigned ct = (unsigned)((H / 4 + 63) / 64);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ct, kColSplits), dim3(512), 0, s, workspace, split, nb, (int)H);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ct, 1), dim3(512), 0, s, split, dw, kColSplits, (int)H);
 }
 
 }  // namespace cs336
