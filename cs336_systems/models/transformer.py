@@ -187,6 +187,8 @@ class CausalMultiHeadSelfAttention(nn.Module):
         self.v_proj = Linear(d_model, num_heads * self.d_v, device, dtype)
         self.output_proj = Linear(num_heads * self.d_v, d_model, device, dtype)
         self.positional_encoder = positional_encoder
+        # (process group, layout) once parallel.context_parallel.enable_context_parallel() is applied
+        self.context_parallel = None
 
     def group_(self) -> None:
         """Store q/k/v projections as one (3*d_model, d_model) block (one QKV GEMM)."""
@@ -210,12 +212,39 @@ class CausalMultiHeadSelfAttention(nn.Module):
         with annotate("attention"):
             return fused.AttentionCore.apply(qkv, cos, sin, p, self.num_heads)
 
+    def _context_parallel_forward(self, x3, token_positions, B, N):
+        """Ring attention over the context-parallel group (``parallel/context_parallel.py``): x3 is
+        this rank's part of the sequence; RoPE uses the tokens' global positions."""
+        from ..parallel.context_parallel import _world_rank, ring_attention, sequence_positions
+
+        group, layout = self.context_parallel
+        H, dk = self.num_heads, self.d_k
+        with annotate("qkv_proj"):
+            q = self.q_proj(x3).view(B, N, H, dk).transpose(1, 2)
+            k = self.k_proj(x3).view(B, N, H, dk).transpose(1, 2)
+            v = self.v_proj(x3).view(B, N, H, dk).transpose(1, 2)
+        if token_positions is None:
+            world, rank = _world_rank(group)
+            pos = sequence_positions(N * world, rank, world, layout, device=x3.device)
+        else:
+            pos = token_positions.reshape(-1, N) if token_positions.numel() != N else token_positions.reshape(N)
+        with annotate("rope"):
+            q = self.positional_encoder(q, pos)
+            k = self.positional_encoder(k, pos)
+        with annotate("ring_attention"):
+            return ring_attention(q, k.to(q.dtype), v.to(q.dtype), group, True, layout)
+
     def forward(self, x: torch.Tensor, token_positions: torch.Tensor | None = None) -> torch.Tensor:
         *b, N, d_model = x.shape
         assert d_model == self.d_model
         B = int(math.prod(b)) if b else 1
         H, dk = self.num_heads, self.d_k
         x3 = x.reshape(B, N, d_model)
+        if self.context_parallel is not None:
+            o = self._context_parallel_forward(x3, token_positions, B, N)
+            o = o.transpose(1, 2).reshape(*b, N, H * dk) if b else o.transpose(1, 2).reshape(N, H * dk)
+            with annotate("out_proj"):
+                return self.output_proj(o)
         if x.is_cuda:
             o = self._fused_path(x3, token_positions, B, N)
             if o is not None:

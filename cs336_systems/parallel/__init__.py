@@ -7,6 +7,15 @@ from .comm import (
     spawn,
     supports_avg,
 )
+from .context_parallel import (
+    RingAttention,
+    disable_context_parallel,
+    enable_context_parallel,
+    ring_attention,
+    sequence_positions,
+    shard_sequence,
+    unshard_sequence,
+)
 from .ddp import DDP, DDP_Bucketed, DDPBucketed, DDPIndividual, DEFAULT_BUCKET_MB, FlatDDP, NaiveDDP
 from .sharded_optimizer import ShardedOptimizer, ShardedStateOptimizer
 
@@ -33,6 +42,13 @@ __all__ = [
     "DDPIndividual",
     "DDP_VARIANTS",
     "DEFAULT_BUCKET_MB",
+    "RingAttention",
+    "disable_context_parallel",
+    "enable_context_parallel",
+    "ring_attention",
+    "sequence_positions",
+    "shard_sequence",
+    "unshard_sequence",
     "FlatDDP",
     "NaiveDDP",
     "ShardedOptimizer",

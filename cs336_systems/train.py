@@ -7,6 +7,9 @@ This driver is one torchrun-compatible entry point over the framework's pieces:
 * model: :func:`cs336_systems.models.build_model` (registry size or explicit dims), bf16 autocast
   over fp32 master weights, HIP kernels on GPU;
 * data parallelism: any of the four DP variants (``--ddp``) and optional ZeRO-1 (``--sharded``);
+* context parallelism (``--context-parallel``, ``--cp-layout zigzag|contiguous``): each sequence is
+  split over the ranks and attention runs as ring attention (``parallel/context_parallel.py``);
+  the DP wrapper still averages the (replicated) weights' gradients;
 * optimizer: fused HIP AdamW (bf16 weight shadows on GPU), cosine LR with warmup, global-norm
   clipping;
 * data: a 1-D token file (``.npy`` or raw ``uint16`` ``.bin``, memory-mapped) or synthetic tokens;
@@ -42,7 +45,15 @@ from . import ops
 from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
 from .models import build_model
 from .models.fused import refresh_bf16_shadows
-from .parallel import DEFAULT_BUCKET_MB, ShardedOptimizer, cleanup_distributed, setup_distributed, wrap_ddp
+from .parallel import (
+    DEFAULT_BUCKET_MB,
+    ShardedOptimizer,
+    cleanup_distributed,
+    enable_context_parallel,
+    setup_distributed,
+    shard_sequence,
+    wrap_ddp,
+)
 
 
 @dataclasses.dataclass
@@ -64,6 +75,8 @@ class TrainConfig:
     ddp: str = "bucketed"
     bucket_mb: float = DEFAULT_BUCKET_MB
     sharded: bool = False
+    context_parallel: bool = False  # split every sequence over the ranks (ring attention) instead of the batch
+    cp_layout: str = "zigzag"
     data: str | None = None  # token file; None = synthetic
     seed: int = 0
     ckpt_dir: str | None = None
@@ -95,15 +108,18 @@ class Batches:
     """Deterministic per-step batches: global batch ``s`` depends only on ``(seed, s)``."""
 
     def __init__(self, cfg: TrainConfig, rank: int, world: int, device: torch.device):
-        if cfg.batch % world:
+        self.cp = cfg.context_parallel and world > 1
+        if cfg.batch % world and not self.cp:
             raise ValueError(f"global batch {cfg.batch} must divide by world size {world}")
-        self.cfg, self.rank, self.local, self.device = cfg, rank, cfg.batch // world, device
+        self.world = world
+        self.cfg, self.rank, self.local, self.device = cfg, rank, (cfg.batch if self.cp else cfg.batch // world), device
         self.tokens = open_tokens(cfg.data) if cfg.data else None
 
     def __call__(self, step: int) -> tuple[torch.Tensor, torch.Tensor]:
         cfg = self.cfg
         g = torch.Generator().manual_seed(cfg.seed * 1_000_003 + step)
-        lo, hi = self.rank * self.local, (self.rank + 1) * self.local
+        # context parallel: every rank takes the whole batch and its part of each sequence
+        lo, hi = (0, cfg.batch) if self.cp else (self.rank * self.local, (self.rank + 1) * self.local)
         if self.tokens is None:
             toks = torch.randint(0, cfg.vocab, (cfg.batch, cfg.ctx + 1), generator=g)[lo:hi]
         else:
@@ -112,7 +128,11 @@ class Batches:
             toks = torch.from_numpy(np.asarray(self.tokens[idx]).astype(np.int64))
         if self.device.type == "cuda":
             toks = toks.pin_memory().to(self.device, non_blocking=True)
-        return toks[:, :-1].contiguous(), toks[:, 1:].contiguous()
+        x, y = toks[:, :-1].contiguous(), toks[:, 1:].contiguous()
+        if self.cp:
+            x = shard_sequence(x, self.rank, self.world, self.cfg.cp_layout)
+            y = shard_sequence(y, self.rank, self.world, self.cfg.cp_layout)
+        return x, y
 
 
 def train(cfg: TrainConfig) -> dict:
@@ -120,6 +140,9 @@ def train(cfg: TrainConfig) -> dict:
     rank, world, dev = setup_distributed(backend="nccl" if use_cuda else "gloo")
     torch.manual_seed(cfg.seed)
     model = build_model(cfg.size, cfg.ctx, vocab_size=cfg.vocab, device=dev)
+    if cfg.context_parallel and world > 1:
+        # sequence split over all ranks; gradients are still averaged over them by the DP wrapper
+        enable_context_parallel(model, None, cfg.cp_layout)
     okw = dict(lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.eps, weight_decay=cfg.wd)
     shadows = dev.type == "cuda" and cfg.dtype == "bf16"
     if cfg.sharded:
