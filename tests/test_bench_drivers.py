@@ -35,3 +35,22 @@ def test_precision_demo():
     acc = precision.accumulation_demo()
     assert abs(acc["fp32 += fp32"] - 10) < 1e-3 and abs(acc["fp16 += fp16"] - 10) > 1e-2
     assert precision.autocast_dtypes(device="cpu")["parameters"] == "torch.float32"
+
+
+@pytest.mark.parametrize(
+    "name",
+    ["benchmark", "benchmark_attention", "ddp_bucketed_overlapped_sharded", "ddp_overlap", "distributed_communication_single",
+     "flash_attention", "flashattentioncode", "mixed_precision_testing", "naive_ddp", "precision", "transformer_annotated"],
+)
+def test_reference_module_paths_import(name):
+    """Every module path of the reference's cs336_systems package exists here."""
+    import importlib
+
+    importlib.import_module(f"cs336_systems.{name}")
+
+
+def test_ddp_overlap_name_is_working_overlapped_ddp():
+    from cs336_systems.ddp_overlap import DDPOverlap
+    from cs336_systems.parallel import DDPIndividual
+
+    assert DDPOverlap is DDPIndividual
