@@ -149,17 +149,25 @@ def compute_weight(params: list[nn.Parameter], dtype: torch.dtype) -> torch.Tens
 # ------------------------------------------------------------------------------------------
 # weight-gradient side stream
 # ------------------------------------------------------------------------------------------
-# dW = dYᵀX is off backward's critical path (nothing in backward consumes it), so it runs on a
+# dW = dYᵀX is off backward's critical path (nothing in backward consumes it), so it CAN run on a
 # second HIP stream while the main stream continues with dX and the memory-bound kernels of the
 # next layers (RMSNorm/SwiGLU/RoPE backward, FA backward). The main stream waits for the side
 # stream only where a weight gradient is consumed: before a DDP bucket / per-parameter all-reduce
 # (sync_dw_stream) and at the end of the backward pass (an engine callback).
+#
+# OFF by default (CS336_DW_STREAM=1 enables it). Measured on MI355X: it saves only ~2 ms of a
+# ~187 ms XL step, because the hipBLASLt GEMMs hold ~1 workgroup per CU and the HBM-bound kernels
+# next to them run 3-5x slower (profiles/r1_overlap_ab.json) — and with the 2.7b shapes at 12288
+# tokens (d_model 2560, d_ff 10240) two hipBLASLt GEMMs running concurrently on the two streams
+# never finished (the step hung in backward; serial streams, or AMD_SERIALIZE_KERNEL=3, complete in
+# 0.15 s). hipBLASLt's stream-K kernels assume they own the device, so concurrent GEMMs are not a
+# safe default.
 _SIDE_STREAMS: dict[int, torch.cuda.Stream] = {}
 _state = {"dirty": False, "callback": False}
 
 
 def dw_stream_enabled() -> bool:
-    return os.environ.get("CS336_DW_STREAM", "1") != "0"
+    return os.environ.get("CS336_DW_STREAM", "0") == "1"
 
 
 def _side_stream(device: torch.device) -> torch.cuda.Stream:
