@@ -57,13 +57,13 @@ def _normalize_pos(pos: torch.Tensor | None, B: int, N: int) -> torch.Tensor | N
 
 
 def _hip_layout_ok(x: torch.Tensor) -> bool:
-    """The kernel moves 16 B per access: contiguous last dim, power-of-two head dim in [8, 256],
+    """The kernel moves 16 B per access: contiguous last dim, head dim a multiple of 8 in [8, 256],
     16-byte aligned base and strides (the fused-QKV slices and fresh tensors always are)."""
     D, es = x.shape[-1], x.element_size()
     return (
         x.stride(-1) == 1
         and 8 <= D <= 256
-        and D & (D - 1) == 0
+        and D % 8 == 0
         and x.data_ptr() % 16 == 0
         and all((x.stride(i) * es) % 16 == 0 for i in range(3))
     )

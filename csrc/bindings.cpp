@@ -421,7 +421,7 @@ void rope_into(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin
   TORCH_CHECK(out.dim() == 4 && out.stride(3) == 1 && out.sizes() == x.sizes() && out.dtype() == x.dtype(),
               "cs336: rope out must match x with contiguous D");
   const int64_t D = x.size(3);
-  TORCH_CHECK(D >= 8 && D <= 256 && (D & (D - 1)) == 0, "cs336: rope head dim must be a power of two in [8, 256]");
+  TORCH_CHECK(D >= 8 && D <= 256 && D % 8 == 0, "cs336: rope head dim must be a multiple of 8 in [8, 256]");
   // 16-B vector accesses: every stride and base 16-B aligned
   const int64_t es = x.element_size();
   for (const at::Tensor* t : {&x, &out}) {

@@ -19,15 +19,15 @@ namespace {
 template <typename T>
 __global__ __launch_bounds__(256) void rope_kernel(const RopeArgs a, const float* __restrict__ cs,
                                                    const float* __restrict__ sn_, const int64_t* __restrict__ pos,
-                                                   int H, int N, int d8_shift, int nchunk, float sgn) {
+                                                   int H, int N, int D8, int nchunk, float sgn) {
   typedef typename Elem<T>::storage S;
   const S* __restrict__ x = (const S*)a.x;
   S* __restrict__ out = (S*)a.out;
-  const int D8 = 1 << d8_shift, half = 4 * D8;
+  const int half = 4 * D8;
   const int t = blockIdx.x / nchunk;  // token
   const int hd = (blockIdx.x - t * nchunk) * 256 + threadIdx.x;
   if (hd >= H * D8) return;
-  const int h = hd >> d8_shift, d8 = hd & (D8 - 1);
+  const int h = hd / D8, d8 = hd - h * D8;  // any D % 8 == 0 (e.g. d_head 80 of the 2.7b model)
   const int b = t / N, n = t - b * N;
   const int64_t p = pos ? pos[t] : (int64_t)n;
   const S* xp = x + b * a.x_sb + h * a.x_sh + n * a.x_sn + 8 * d8;
@@ -52,21 +52,20 @@ __global__ __launch_bounds__(256) void rope_kernel(const RopeArgs a, const float
 
 void rope(const RopeArgs& a, DType t, const float* cos_, const float* sin_, const int64_t* pos, int B, int H, int N,
           int D, bool inverse, hipStream_t s) {
-  // D % 8 == 0 and D/8 a power of two (head dims 8 .. 256); the binding checks it
-  int shift = 0;
-  while ((8 << shift) < D) ++shift;
-  const int nchunk = (H * (D / 8) + 255) / 256;
+  // D % 8 == 0 (head dims 8 .. 256); the binding checks it
+  const int D8 = D / 8;
+  const int nchunk = (H * D8 + 255) / 256;
   const dim3 grid((unsigned)((int64_t)B * N * nchunk)), block(256);
   const float sgn = inverse ? -1.f : 1.f;
   switch (t) {
     case DType::F32:
-      hipLaunchKernelGGL(rope_kernel<float>, grid, block, 0, s, a, cos_, sin_, pos, H, N, shift, nchunk, sgn);
+      hipLaunchKernelGGL(rope_kernel<float>, grid, block, 0, s, a, cos_, sin_, pos, H, N, D8, nchunk, sgn);
       break;
     case DType::BF16:
-      hipLaunchKernelGGL(rope_kernel<BF16>, grid, block, 0, s, a, cos_, sin_, pos, H, N, shift, nchunk, sgn);
+      hipLaunchKernelGGL(rope_kernel<BF16>, grid, block, 0, s, a, cos_, sin_, pos, H, N, D8, nchunk, sgn);
       break;
     case DType::F16:
-      hipLaunchKernelGGL(rope_kernel<F16>, grid, block, 0, s, a, cos_, sin_, pos, H, N, shift, nchunk, sgn);
+      hipLaunchKernelGGL(rope_kernel<F16>, grid, block, 0, s, a, cos_, sin_, pos, H, N, D8, nchunk, sgn);
       break;
   }
 }

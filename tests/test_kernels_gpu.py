@@ -44,7 +44,7 @@ def test_rmsnorm(H, xdt, odt):
 # ---------------------------------------------------------------------------------- RoPE
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("with_pos", [False, True])
-@pytest.mark.parametrize("D", [32, 64, 128])
+@pytest.mark.parametrize("D", [32, 64, 80, 128])
 def test_rope(dt, with_pos, D):
     torch.manual_seed(0)
     B, N, H, ctx = 2, 33, 3, 64
