@@ -1,0 +1,86 @@
+"""Achieved throughput of every hot kernel of one training step vs the MI355X roofline, from a
+rocprofv3 kernel trace of ``bench.py`` (default: XL, ctx 512, batch 24, bf16).
+
+    python scripts/roofline_table.py <run>_kernel_trace.csv [--d 1600 --ff 6400 --layers 48 --heads 25 --batch 24 --ctx 512]
+
+Bytes per element follow the kernels' actual dtypes (fp32 residual stream, bf16 activations, fp32
+master weights/optimizer state, bf16 shadows). Peaks: 2.5 PF/s dense bf16 MFMA (spec) and
+6.3 TB/s (the measured float4-copy HBM rate of MI355X_MICROARCH.md; 8 TB/s spec).
+"""
+
+import argparse
+import csv
+import re
+from collections import defaultdict
+
+PEAK_TF, PEAK_TBS = 2500.0, 6.3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--d", type=int, default=1600)
+    ap.add_argument("--ff", type=int, default=6400)
+    ap.add_argument("--layers", type=int, default=48)
+    ap.add_argument("--heads", type=int, default=25)
+    ap.add_argument("--batch", type=int, default=24)
+    ap.add_argument("--ctx", type=int, default=512)
+    ap.add_argument("--vocab", type=int, default=10000)
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    starts = [s for s, _, n in iv if "vectorized_gather_kernel" in n]
+    lo, hi = starts[-2], starts[-1]
+    step = [x for x in iv if lo <= x[0] < hi]
+    t = defaultdict(float)
+    n = defaultdict(int)
+    xf = [s for s, _, k in step if "xent_fwd" in k][0]
+    for s, e, k in step:
+        if k.startswith("Cijk") or k.startswith("Custom_Cijk"):
+            key = "GEMM fwd" if s < xf else "GEMM bwd (dX + dW)"
+        elif "fa_fwd" in k:
+            key = "FA fwd"
+        elif "fa_bwd" in k:
+            key = "FA bwd (dq + dkdv)"
+        else:
+            m = re.search(r"(\w+_kernel)\b", k)
+            key = m.group(1) if m else k.split("(")[0][:40]
+        t[key] += (e - s) / 1e6
+        n[key] += 1
+    M, d, f, L, H, N, B, V = a.batch * a.ctx, a.d, a.ff, a.layers, a.heads, a.ctx, a.batch, a.vocab
+    P = L * (4 * d * d + 3 * d * f + 2 * d) + 2 * V * d + d
+    gemm_fwd = 2 * M * L * (4 * d * d + 3 * d * f) + 2 * M * d * V
+    attn_fwd = 4 * B * H * N * N * (d // H) / 2
+    work = {  # kernel -> (kind, amount): FLOPs or bytes for the whole step
+        "GEMM fwd": ("F", gemm_fwd),
+        "GEMM bwd (dX + dW)": ("F", 2 * gemm_fwd),
+        "FA fwd": ("F", L * attn_fwd),
+        "FA bwd (dq + dkdv)": ("F", L * 2.5 * attn_fwd),
+        "rmsnorm_fwd_kernel": ("B", 2 * L * M * d * 12),  # x f32 + r bf16 in, s f32 + y bf16 out
+        "rmsnorm_bwd_kernel": ("B", 2 * L * M * d * 16),  # dy bf16, x f32, dres f32 in; dx f32 + bf16 out
+        "silu_mul_fwd_kernel": ("B", L * M * f * 6),
+        "silu_mul_bwd_kernel": ("B", L * M * f * 10),
+        "rope_kernel": ("B", 2 * L * M * 2 * d * 4),
+        "adamw_kernel": ("B", P * 30),  # p,g,m,v in; p,m,v + bf16 shadow out
+        "transpose16_kernel": ("B", None),
+    }
+    total = sum(t.values())
+    print(f"step window {(hi - lo) / 1e6:.1f} ms, kernel time {total:.1f} ms\n")
+    print("| kernel | calls | ms/step | achieved | roofline | % of roofline |")
+    print("|---|---|---|---|---|---|")
+    for k, ms in sorted(t.items(), key=lambda x: -x[1]):
+        if ms < 0.3:
+            continue
+        kind, amt = work.get(k, (None, None))
+        if kind == "F":
+            ach = amt / (ms * 1e-3) / 1e12
+            print(f"| {k} | {n[k]} | {ms:.1f} | {ach:.0f} TFLOP/s | {PEAK_TF:.0f} TFLOP/s dense bf16 | {100 * ach / PEAK_TF:.0f} % |")
+        elif kind == "B" and amt:
+            ach = amt / (ms * 1e-3) / 1e12
+            print(f"| {k} | {n[k]} | {ms:.1f} | {ach:.2f} TB/s | {PEAK_TBS} TB/s HBM | {100 * ach / PEAK_TBS:.0f} % |")
+        else:
+            print(f"| {k} | {n[k]} | {ms:.1f} | | | |")
+
+
+if __name__ == "__main__":
+    main()
