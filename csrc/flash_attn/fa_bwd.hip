@@ -239,18 +239,19 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
 // ============================================================================================
 // dK / dV kernel
 // ============================================================================================
-// Occupancy hint: D=64 asks for two workgroups per CU explicitly (same occupancy as without the hint,
-// but the register schedule it produces measured 4-7 % faster at N=512 and 4096); at D=128 the hint
-// spills the resident K/V fragments (1153 -> 1461 us at N=4096), so D=128 runs one per CU.
+// Occupancy hint: 16-bit D=64 asks for two workgroups per CU explicitly (same occupancy as without
+// the hint, but the register schedule it produces measured 2-5 % faster at N=512 and 4096); at D=128
+// the hint spills the resident K/V fragments (1153 -> 1461 us at N=4096), so D=128 runs one per CU.
 template <typename T, int D, bool CAUSAL, bool ROPE>
-__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fa_bwd_dkdv_kernel(const AttnBwdParams bp) {
+__global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 2 : 1) void fa_bwd_dkdv_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
   const AttnParams p = bp.f;  // by value: a reference would spill the kernarg struct to scratch
   constexpr bool F32 = std::is_same<T, float>::value;
   constexpr int ES = sizeof(S);
   constexpr int RB = D * ES, CPR = RB / 16, EPC = 16 / ES;
-  // D=128 streams 32-query tiles (register budget: resident K/V fragments + dK/dV accumulators)
-  constexpr int BK = 128, BQ = D == 128 ? 32 : 64;
+  // 64-query tiles; at D=128 (one workgroup per CU anyway) part of the state lives in AGPRs
+  // rather than halving the tile: 1153 -> 1046 us at N=4096 (fp32 keeps 32-query tiles)
+  constexpr int BK = 128, BQ = (D == 128 && std::is_same<T, float>::value) ? 32 : 64;
   constexpr int NT = BQ / 32;
   constexpr int TILE = BQ * RB;
   constexpr int BUF = 2 * TILE + 2 * BQ * 4;  // Q, dO images + L2, delta rows
