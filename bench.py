@@ -68,6 +68,7 @@ def parse(argv=None):
         # the GPU 97 % busy, so the HBM-bound update only competes with the GEMMs (profiles/README.md)
         help="run the AdamW update during backward on a side stream (auto: on GPU when clip == 0 and not sharded)",
     )
+    ap.add_argument("--graphs", action="store_true", help="1 GPU: replay forward+backward from one captured HIP graph")
     ap.add_argument(
         "--tunableop",
         default="auto",
@@ -165,8 +166,22 @@ def main(argv=None):
         # unset grads: the projection GEMMs then write fp32 dW straight into the DDP buckets
         opt.zero_grad(set_to_none=True)
 
+    graphed = None
+    if args.graphs and world == 1 and device.type == "cuda":
+        from cs336_systems.utils.graphs import GraphedStep
+
+        def loss_fn(xs, ys):
+            with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
+                return ops.cross_entropy(ddp_model(xs), ys)
+
+        graphed = GraphedStep(loss_fn, model.parameters(), *batches[0])
+
     def step(i):
         x, y = batches[i % len(batches)]
+        if graphed is not None:  # captured forward + loss + backward, eager AdamW
+            loss = graphed(x, y)
+            opt.step()
+            return loss
         zero_grads()
         with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
             logits = ddp_model(x)
@@ -237,6 +252,7 @@ def main(argv=None):
             "bucket_mb": (args.bucket_mb if args.bucket_mb is not None else DEFAULT_BUCKET_MB) if world > 1 else None,
             "optimizer": "fused HIP AdamW (fp32 master weights)" + (", overlapped with backward" if overlap else ""),
             "attention": "HIP FlashAttention-2 (causal)",
+            "hip_graph": graphed is not None,
         },
         "mfu_dense_bf16": round(mfu, 4),
         "model_tflops_per_gpu": round(value * flops_tok / world / 1e12, 1),

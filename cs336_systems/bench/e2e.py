@@ -60,6 +60,7 @@ def run_simple_benchmark(
     optimizer: str = "fused",
     memory_snapshot: str | None = None,
     attention: str = "auto",
+    graphs: bool = False,
 ) -> dict:
     from ..models import set_attention_impl
 
@@ -89,13 +90,28 @@ def run_simple_benchmark(
         opt.step()
         return loss
 
+    if graphs:
+        # forward + loss + backward replayed from one HIP graph; AdamW runs eagerly after it
+        from ..utils.graphs import GraphedStep
+
+        def loss_fn(xs, ys):
+            with ctx():
+                return ops.cross_entropy(fmodel(xs), ys)
+
+        gstep = GraphedStep(loss_fn, model.parameters(), x, y)
+
+        def full():  # noqa: F811
+            loss = gstep(x, y)
+            opt.step()
+            return loss
+
     for _ in range(warmup_steps):
         full()
     _sync(dev)
     reset_peak(dev)
     rec = {"fwd": [], "bwd": [], "opt": [], "step": []}
     with record_memory_history(memory_snapshot):
-        for _ in range(timed_steps):
+        for _ in range(0 if graphs else timed_steps):  # a graph replays fwd+bwd as one unit
             opt.zero_grad(set_to_none=True)
             t, loss = _ms(fwd, dev)
             rec["fwd"].append(t)
@@ -106,9 +122,9 @@ def run_simple_benchmark(
         for _ in range(timed_steps):
             t, _ = _ms(full, dev)
             rec["step"].append(t)
-    out = dict(size=size, ctx=context_length, batch=batch_size, mixed=mixed_precision, compile=compile, attention=attention)
+    out = dict(size=size, ctx=context_length, batch=batch_size, mixed=mixed_precision, compile=compile, attention=attention, graphs=graphs)
     for k, v in rec.items():
-        out[f"{k}_ms"] = statistics.fmean(v)
+        out[f"{k}_ms"] = statistics.fmean(v) if v else float("nan")
         out[f"{k}_std"] = statistics.pstdev(v) if len(v) > 1 else 0.0
     toks = batch_size * context_length
     out["tokens_per_s"] = toks / (out["step_ms"] / 1e3)
@@ -160,6 +176,7 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--mixed", action="store_true")
     ap.add_argument("--compile", action="store_true")
+    ap.add_argument("--graphs", action="store_true", help="replay forward+backward from one captured HIP graph")
     ap.add_argument("--optimizer", default="fused", choices=["fused", "reference"])
     ap.add_argument("--attention", default="auto", choices=["auto", "naive", "flash"])
     ap.add_argument("--memory", action="store_true", help="memory profile (forward and fullstep) instead of timing")
@@ -177,7 +194,7 @@ def main(argv=None):
                             snap = f"{a.snapshot_dir}/memory_{size}_ctx{ctx}_{mode}_{'mixed' if a.mixed else 'fp32'}.pickle"
                         rows.append(dict(size=size, ctx=ctx, mode=mode, mixed=a.mixed, peak_mib=run_memory_profile(size, ctx, mode, a.mixed, a.batch, snap)))
                 else:
-                    rows.append(run_simple_benchmark(size, ctx, a.batch, a.warmup, a.steps, a.mixed, a.compile, optimizer=a.optimizer, attention=a.attention))
+                    rows.append(run_simple_benchmark(size, ctx, a.batch, a.warmup, a.steps, a.mixed, a.compile, optimizer=a.optimizer, attention=a.attention, graphs=a.graphs))
             except torch.OutOfMemoryError:
                 rows.append(dict(size=size, ctx=ctx, error="OOM"))
             torch.cuda.empty_cache() if torch.cuda.is_available() else None

@@ -269,7 +269,10 @@ class FusedLinearFn(torch.autograd.Function):
         # are K-major, which hipBLASLt runs 1.15-1.4x faster (profiles/r1_gemm_dw_layouts.json).
         # Wᵀ is made on the side stream right here, off the forward's critical path.
         ctx.wt_event = None
-        if x2.is_cuda and ctx.needs_input_grad[0] and w.dtype == torch.bfloat16 and _transpose_weight():
+        ctx.w_t = x2.is_cuda and ctx.needs_input_grad[0] and w.dtype == torch.bfloat16 and _transpose_weight()
+        if ctx.w_t and torch.cuda.is_current_stream_capturing():
+            w_saved = _transpose(w)  # inside a HIP-graph capture: stay on the capturing stream
+        elif ctx.w_t:
             main = torch.cuda.current_stream(x2.device)
             s = _side_stream(x2.device)
             s.wait_stream(main)
@@ -306,10 +309,11 @@ class FusedLinearFn(torch.autograd.Function):
             dy2 = dy2.to(w.dtype)
         dx = dw_parts = None
         if ctx.needs_input_grad[0]:
-            if ctx.wt_event is not None:  # w holds Wᵀ (K_in, N_out), made on the side stream
-                main = torch.cuda.current_stream(dy2.device)
-                main.wait_event(ctx.wt_event)
-                w.record_stream(main)
+            if ctx.w_t:  # w holds Wᵀ (K_in, N_out), made on the side stream (or in-stream under capture)
+                if ctx.wt_event is not None:
+                    main = torch.cuda.current_stream(dy2.device)
+                    main.wait_event(ctx.wt_event)
+                    w.record_stream(main)
                 dx = gemm.mm_nt(dy2, w).view(ctx.x_shape)
             else:
                 dx = gemm.mm_nn(dy2, w).view(ctx.x_shape)

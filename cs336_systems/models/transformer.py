@@ -73,6 +73,26 @@ class Linear(nn.Module):
         return f"d_out={self.weight.shape[0]}, d_in={self.weight.shape[1]}"
 
 
+class _GraphSafeEmbedding(torch.autograd.Function):
+    """Embedding lookup whose backward is one atomic ``index_add_`` into a zeroed table. ATen's
+    embedding backward sorts and partitions the token ids with data-dependent sizes; replaying a
+    HIP graph captured around it faulted in rocprim's partition kernel at the XL shape, so this op
+    is used while a graph is being captured (``utils/graphs.py``)."""
+
+    @staticmethod
+    def forward(ctx, ids, weight):
+        ctx.save_for_backward(ids)
+        ctx.wshape, ctx.wdtype = weight.shape, weight.dtype
+        return F.embedding(ids, weight)
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids,) = ctx.saved_tensors
+        gw = torch.zeros(ctx.wshape, dtype=torch.float32, device=g.device)
+        gw.index_add_(0, ids.reshape(-1), g.reshape(-1, ctx.wshape[1]).float())
+        return None, gw if ctx.wdtype == torch.float32 else gw.to(ctx.wdtype)
+
+
 class Embedding(nn.Module):
     """Token embedding table ``(vocab, d_model)``, trunc-normal std 1 (``model.py:47-60``)."""
 
@@ -81,6 +101,8 @@ class Embedding(nn.Module):
         self.weight = nn.Parameter(_trunc_normal((vocab_size, d_model), 1.0, device, dtype), requires_grad=True)
 
     def forward(self, token_ids: torch.Tensor) -> torch.Tensor:
+        if token_ids.is_cuda and torch.cuda.is_current_stream_capturing():
+            return _GraphSafeEmbedding.apply(token_ids, self.weight)
         return F.embedding(token_ids, self.weight)
 
     def extra_repr(self):
