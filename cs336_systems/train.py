@@ -10,6 +10,8 @@ This driver is one torchrun-compatible entry point over the framework's pieces:
 * context parallelism (``--context-parallel``, ``--cp-layout zigzag|contiguous``): each sequence is
   split over the ranks and attention runs as ring attention (``parallel/context_parallel.py``);
   the DP wrapper still averages the (replicated) weights' gradients;
+* HIP graphs (``--graphs``, single process on GPU): forward + loss + backward replayed from one
+  captured graph (``utils/graphs.py``), the optimizer stepping eagerly after each replay;
 * optimizer: fused HIP AdamW (bf16 weight shadows on GPU), cosine LR with warmup, global-norm
   clipping;
 * data: a 1-D token file (``.npy`` or raw ``uint16`` ``.bin``, memory-mapped) or synthetic tokens;
@@ -77,6 +79,7 @@ class TrainConfig:
     sharded: bool = False
     context_parallel: bool = False  # split every sequence over the ranks (ring attention) instead of the batch
     cp_layout: str = "zigzag"
+    graphs: bool = False  # single process on GPU: replay fwd + loss + bwd from one captured HIP graph
     data: str | None = None  # token file; None = synthetic
     seed: int = 0
     ckpt_dir: str | None = None
@@ -159,8 +162,11 @@ def train(cfg: TrainConfig) -> dict:
             refresh_bf16_shadows(model.parameters())
             if rank == 0:
                 print(f"resumed from {path} at step {start}", flush=True)
-    # DDP wraps after loading so its initial broadcast ships the restored weights
-    ddp = wrap_ddp(model, cfg.ddp, bucket_size_mb=cfg.bucket_mb)
+    # DDP wraps after loading so its initial broadcast ships the restored weights. A HIP-graph run
+    # (single process) trains the bare model: the captured backward has no collectives to issue.
+    use_graphs = cfg.graphs and world == 1 and dev.type == "cuda"
+    ddp = model if use_graphs else wrap_ddp(model, cfg.ddp, bucket_size_mb=cfg.bucket_mb)
+    graphed = None
     batches = Batches(cfg, rank, world, dev)
     amp = dev.type == "cuda" and cfg.dtype == "bf16"
     autocast = (lambda: torch.autocast("cuda", dtype=torch.bfloat16)) if amp else contextlib.nullcontext
@@ -174,14 +180,25 @@ def train(cfg: TrainConfig) -> dict:
         for g in opt.param_groups:
             g["lr"] = lr
         x, y = batches(step)
-        if hasattr(ddp, "zero_grad") and cfg.ddp in ("bucketed", "flat"):
-            ddp.zero_grad()
+        if use_graphs:
+            if graphed is None:
+                from .utils.graphs import GraphedStep
+
+                def loss_fn(xs, ys):
+                    with autocast():
+                        return ops.cross_entropy(model(xs), ys)
+
+                graphed = GraphedStep(loss_fn, model.parameters(), x, y)
+            loss = graphed(x, y)  # gradients land in the graph's static tensors, re-attached to .grad
         else:
-            opt.zero_grad(set_to_none=True)
-        with autocast():
-            loss = ops.cross_entropy(ddp(x), y)
-        loss.backward()
-        ddp.finish_gradient_synchronization()
+            if hasattr(ddp, "zero_grad") and cfg.ddp in ("bucketed", "flat"):
+                ddp.zero_grad()
+            else:
+                opt.zero_grad(set_to_none=True)
+            with autocast():
+                loss = ops.cross_entropy(ddp(x), y)
+            loss.backward()
+            ddp.finish_gradient_synchronization()
         gnorm = ops.clip_grad_norm_(model.parameters(), cfg.clip) if cfg.clip > 0 else None
         opt.step()
         tok_since += cfg.batch * cfg.ctx

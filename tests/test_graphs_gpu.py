@@ -79,3 +79,22 @@ def test_graph_replay_with_different_token_sets():
 def test_e2e_benchmark_graphs_mode():
     row = e2e.run_simple_benchmark("small", 128, 2, warmup_steps=2, timed_steps=3, mixed_precision=True, graphs=True)
     assert row["graphs"] and row["step_ms"] > 0
+
+
+def test_train_driver_graphs(tmp_path):
+    from cs336_systems.train import TrainConfig, train
+
+    import os
+
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1")
+    from cs336_systems.parallel.comm import cleanup_distributed, find_free_port
+
+    os.environ["MASTER_PORT"] = str(find_free_port())
+    cfg = TrainConfig(size="tiny", ctx=64, vocab=500, batch=4, steps=4, warmup=1, lr=1e-3, clip=1.0, graphs=True,
+                      device="cuda", log_every=1, ckpt_dir=str(tmp_path / "ck"))
+    try:
+        out = train(cfg)
+    finally:
+        cleanup_distributed()
+    losses = [h["loss"] for h in out["history"]]
+    assert len(losses) == 4 and all(0 < v < 10 for v in losses)
