@@ -126,22 +126,29 @@ def _merge(acc_o: list, acc_l: list, i: int, o: torch.Tensor, lse: torch.Tensor)
     acc_l[i] = m + torch.log(s)
 
 
-def _ring_pass(tensors: list[torch.Tensor], group):
-    """Send ``tensors`` to the next rank and receive the previous rank's into fresh buffers.
-    Returns (requests, buffers); buffers are valid after every request has been waited on."""
-    world, rank = _world_rank(group)
-    nxt, prv = (rank + 1) % world, (rank - 1) % world
-    if group is not None:
-        nxt, prv = dist.get_global_rank(group, nxt), dist.get_global_rank(group, prv)
-    bufs = [torch.empty_like(t) for t in tensors]
-    ops = [dist.P2POp(dist.isend, t, nxt, group) for t in tensors]
-    ops += [dist.P2POp(dist.irecv, b, prv, group) for b in bufs]
-    return dist.batch_isend_irecv(ops), bufs
+class _RingXfer:
+    """Send ``tensors`` to the next rank and receive the previous rank's (P2P, in flight until
+    :meth:`wait`, which returns the received tensors). With gloo and GPU tensors (the one-GPU
+    multi-rank rehearsal) the transfer is staged through host memory explicitly, so it is ordered
+    with the kernels that produce and consume the buffers."""
 
+    def __init__(self, tensors: list[torch.Tensor], group):
+        world, rank = _world_rank(group)
+        nxt, prv = (rank + 1) % world, (rank - 1) % world
+        if group is not None:
+            nxt, prv = dist.get_global_rank(group, nxt), dist.get_global_rank(group, prv)
+        self.device = tensors[0].device
+        self.staged = tensors[0].is_cuda and dist.get_backend(group) == "gloo"
+        send = [t.cpu() for t in tensors] if self.staged else tensors
+        self.bufs = [torch.empty_like(t) for t in send]
+        ops = [dist.P2POp(dist.isend, t, nxt, group) for t in send]
+        ops += [dist.P2POp(dist.irecv, b, prv, group) for b in self.bufs]
+        self.reqs = dist.batch_isend_irecv(ops)
 
-def _wait(reqs) -> None:
-    for r in reqs or ():
-        r.wait()
+    def wait(self) -> list[torch.Tensor]:
+        for r in self.reqs:
+            r.wait()
+        return [b.to(self.device) for b in self.bufs] if self.staged else self.bufs
 
 
 class RingAttention(torch.autograd.Function):
@@ -166,7 +173,7 @@ class RingAttention(torch.autograd.Function):
         cur_k, cur_v = k, v
         for step in range(world):
             src = (rank - step) % world
-            reqs, nxt = _ring_pass([cur_k, cur_v], group) if step + 1 < world else (None, None)
+            xfer = _RingXfer([cur_k, cur_v], group) if step + 1 < world else None
             theirs = _sub_ids(src, world, layout)
             for qi in range(S):
                 for kj in range(S):
@@ -178,9 +185,8 @@ class RingAttention(torch.autograd.Function):
                         cur_v[:, :, kj * c : (kj + 1) * c], causal and gk == gq, scale,
                     )
                     _merge(acc_o, acc_l, qi, o, lse)
-            if reqs is not None:
-                _wait(reqs)
-                cur_k, cur_v = nxt
+            if xfer is not None:
+                cur_k, cur_v = xfer.wait()
         out = torch.cat([a.to(q.dtype) for a in acc_o], dim=2) if S > 1 else acc_o[0].to(q.dtype)
         ctx.save_for_backward(q, k, v, out, *[l.contiguous() for l in acc_l])
         ctx.group, ctx.causal, ctx.layout, ctx.scale = group, causal, layout, scale
@@ -202,7 +208,7 @@ class RingAttention(torch.autograd.Function):
         cur_dv = torch.zeros(v.shape, dtype=torch.float32, device=v.device)
         for step in range(world):
             src = (rank - step) % world
-            kv_reqs, kv_nxt = _ring_pass([cur_k, cur_v], group) if step + 1 < world else (None, None)
+            kv_xfer = _RingXfer([cur_k, cur_v], group) if step + 1 < world else None
             theirs = _sub_ids(src, world, layout)
             for qi in range(S):
                 qs = slice(qi * c, (qi + 1) * c)
@@ -219,12 +225,9 @@ class RingAttention(torch.autograd.Function):
                     cur_dk[:, :, ks] += dk_p.float()
                     cur_dv[:, :, ks] += dv_p.float()
             if world > 1:  # the visiting chunk's gradients move on with it; the last hop returns them home
-                g_reqs, g_nxt = _ring_pass([cur_dk, cur_dv], group)
-                _wait(g_reqs)
-                cur_dk, cur_dv = g_nxt
-            if kv_reqs is not None:
-                _wait(kv_reqs)
-                cur_k, cur_v = kv_nxt
+                cur_dk, cur_dv = _RingXfer([cur_dk, cur_dv], group).wait()
+            if kv_xfer is not None:
+                cur_k, cur_v = kv_xfer.wait()
         return dq.to(q.dtype), cur_dk.to(k.dtype), cur_dv.to(v.dtype), None, None, None
 
 

@@ -68,3 +68,16 @@ def test_context_parallel_lm_world1_matches_plain():
     torch.testing.assert_close(loss_cp, loss_ref, rtol=1e-2, atol=1e-2)
     for n in g_ref:
         torch.testing.assert_close(g_cp[n], g_ref[n], rtol=5e-2, atol=5e-3, msg=n)
+
+
+@pytest.mark.parametrize("world,layout", [(2, "zigzag"), (4, "contiguous"), (4, "zigzag")])
+def test_ring_attention_multirank_one_gpu(world, layout):
+    """2-4 ranks share cuda:0 (gloo, host-staged P2P): the multi-hop ring on the HIP kernels."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "cp_gloo_gpu.py"), "--layout", layout, "--world", str(world)],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.count("matches full HIP FA2") == world
