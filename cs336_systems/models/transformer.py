@@ -275,9 +275,16 @@ class CausalMultiHeadSelfAttention(nn.Module):
                     return self.output_proj(o)
         # (B, N, H, dk) memory, viewed as (B, H, N, dk): no transpose copies on the GPU path
         with annotate("qkv_proj"):
-            q = self.q_proj(x3).view(B, N, H, dk).transpose(1, 2)
-            k = self.k_proj(x3).view(B, N, H, dk).transpose(1, 2)
-            v = self.v_proj(x3).view(B, N, H, dk).transpose(1, 2)
+            w = [self.q_proj.weight, self.k_proj.weight, self.v_proj.weight]
+            if x.is_cuda and fused.grouped_view(w) is not None:
+                # head dims the fused attention core does not take (e.g. 80 in the 2.7b model) still
+                # get the single grouped QKV GEMM; q/k/v are strided views of its output
+                qkv = fused.fused_linear(x3, *w).view(B, N, 3, H, dk)
+                q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))
+            else:
+                q = self.q_proj(x3).view(B, N, H, dk).transpose(1, 2)
+                k = self.k_proj(x3).view(B, N, H, dk).transpose(1, 2)
+                v = self.v_proj(x3).view(B, N, H, dk).transpose(1, 2)
         pos = token_positions
         if pos is not None:
             pos = pos.reshape(-1, N) if pos.numel() != N else pos.reshape(N)

@@ -262,12 +262,15 @@ def test_swiglu_fused_matches_reference():
 
 
 @pytest.mark.parametrize("amp", [False, True])
-def test_fused_layout_matches_unfused(amp):
-    """Grouped QKV / W1|W3 GEMMs + AttentionCore + fp32-out dW == the unfused GPU path."""
+@pytest.mark.parametrize("heads", [4, 2])
+def test_fused_layout_matches_unfused(amp, heads):
+    """Grouped QKV / W1|W3 GEMMs + AttentionCore + fp32-out dW == the unfused GPU path; heads=2 gives
+    d_head 80 (the 2.7b model's), where the grouped QKV GEMM feeds padded FA2 through strided views."""
     from cs336_systems.models import BasicsTransformerLM
 
     torch.manual_seed(0)
-    cfg = dict(vocab_size=500, context_length=128, d_model=256, num_layers=2, num_heads=4, d_ff=512, rope_theta=10000.0)
+    d = 256 if heads == 4 else 160
+    cfg = dict(vocab_size=500, context_length=128, d_model=d, num_layers=2, num_heads=heads, d_ff=512, rope_theta=10000.0)
     m_f = BasicsTransformerLM(**cfg, device=DEV, fused_layout=True)
     m_u = BasicsTransformerLM(**cfg, device=DEV, fused_layout=False)
     m_u.load_state_dict(m_f.state_dict())
