@@ -422,6 +422,7 @@ void rope_into(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin
               "cs336: rope out must match x with contiguous D");
   const int64_t D = x.size(3);
   TORCH_CHECK(D >= 8 && D <= 256 && D % 8 == 0, "cs336: rope head dim must be a multiple of 8 in [8, 256]");
+  TORCH_CHECK(x.size(0) * x.size(1) * x.size(2) * (D / 8) < ((int64_t)1 << 31), "cs336: rope tensor too large for 32-bit indexing");
   // 16-B vector accesses: every stride and base 16-B aligned
   const int64_t es = x.element_size();
   for (const at::Tensor* t : {&x, &out}) {
