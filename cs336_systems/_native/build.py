@@ -48,7 +48,8 @@ def _hipcc():
 
 def _sources():
     kernels = sorted(glob.glob(os.path.join(CSRC, "**", "*.hip"), recursive=True))
-    host = [os.path.join(CSRC, "bindings.cpp")]
+    # host-only TUs (torch headers): the op bindings and the hipBLASLt autotuner (csrc/blas)
+    host = [os.path.join(CSRC, "bindings.cpp")] + sorted(glob.glob(os.path.join(CSRC, "blas", "*.cpp")))
     return kernels, host
 
 
@@ -135,6 +136,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
             "-ltorch",
             "-ltorch_cpu",
             "-ltorch_hip",
+            # torch's bundled hipBLASLt (the same library and handle torch.mm uses)
+            "-lhipblaslt",
             "-Wl,-rpath," + torch_lib,
         ]
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -6,6 +6,12 @@ DDP bucket) through the cs336 kernel; the default ``blas`` keeps hipBLASLt, whic
 on the XL shapes in round 1 (``profiles/r1_gemm_cs336_vs_hipblaslt.json``: the cs336 kernel reaches
 60-100 % of hipBLASLt's TFLOPS; hipBLASLt picks stream-K 160×256 Tensile kernels for these shapes).
 Unsupported shapes (tile divisibility, K % 64) always fall back to ``torch.mm``.
+
+``CS336_GEMM=lt`` routes the same GEMMs through ``cs336::lt_gemm`` (``csrc/blas/lt_gemm.cpp``):
+hipBLASLt with per-problem autotuning over the heuristic's top candidates (``CS336_LT_CANDIDATES``,
+default 48), fp32 output included, which TunableOp does not cover. On the XL shapes the tuned pick
+is within noise of ``torch.mm``'s on most GEMMs and 1.1-1.5x faster on a few fp32-output weight
+gradients (``profiles/r1_lt_gemm_sweep*.json``), so ``blas`` stays the default.
 """
 
 from __future__ import annotations
@@ -21,12 +27,22 @@ def hip_gemm_enabled() -> bool:
     return os.environ.get("CS336_GEMM", "blas").lower() == "hip" and ext_available()
 
 
+def lt_gemm_enabled() -> bool:
+    return os.environ.get("CS336_GEMM", "blas").lower() == "lt" and ext_available()
+
+
+def _lt_ok(*ts) -> bool:
+    return all(t.is_cuda and t.dim() == 2 and t.stride(1) == 1 for t in ts) and ts[0].dtype == torch.bfloat16 and ts[1].dtype == torch.bfloat16
+
+
 def _ok(a, b, ta, tb) -> bool:
     return a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and ops().gemm_ok(a, b, ta, tb)
 
 
 def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``x @ w.T`` (forward of a linear layer)."""
+    if lt_gemm_enabled() and _lt_ok(x, w):
+        return ops().lt_gemm(x, w, False, True, torch.bfloat16)
     if hip_gemm_enabled() and _ok(x, w, False, True):
         return ops().gemm(x, w, False, True, torch.bfloat16, 0, 0, 0)
     return torch.mm(x, w.t())
@@ -34,6 +50,8 @@ def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 def mm_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``dy @ w`` (input gradient)."""
+    if lt_gemm_enabled() and _lt_ok(dy, w):
+        return ops().lt_gemm(dy, w, False, False, torch.bfloat16)
     if hip_gemm_enabled() and _ok(dy, w, False, False):
         return ops().gemm(dy, w, False, False, torch.bfloat16, 0, 0, 0)
     return torch.mm(dy, w)
@@ -42,6 +60,11 @@ def mm_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """``dy.T @ xt.T`` with an fp32 result: the weight gradient from a token-contiguous ``Xᵀ``
     (K_in, tokens). hipBLASLt only: its NT kernels are the fast ones for this layout."""
+    if lt_gemm_enabled() and _lt_ok(dy, xt) and (out is None or out.stride(1) == 1):
+        if out is None:
+            return ops().lt_gemm(dy, xt, True, True, torch.float32)
+        ops().lt_gemm_out(dy, xt, True, True, out)
+        return out
     if out is not None:
         torch.mm(dy.t(), xt.t(), out_dtype=torch.float32, out=out)
         return out
@@ -50,6 +73,11 @@ def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None =
 
 def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """``dy.T @ x`` with an fp32 result (weight gradient), written into ``out`` when given."""
+    if lt_gemm_enabled() and _lt_ok(dy, x) and (out is None or out.stride(1) == 1):
+        if out is None:
+            return ops().lt_gemm(dy, x, True, False, torch.float32)
+        ops().lt_gemm_out(dy, x, True, False, out)
+        return out
     if hip_gemm_enabled() and _ok(dy, x, True, False):
         if out is not None:
             ops().gemm_out(dy, x, True, False, out, False, 0, 0, 0)

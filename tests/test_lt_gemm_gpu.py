@@ -1,0 +1,103 @@
+"""Autotuned hipBLASLt GEMM (``cs336::lt_gemm``, csrc/blas/lt_gemm.cpp) against an fp32 PyTorch
+reference in every transpose combination and both output dtypes, strided (non-contiguous row
+stride) operands and outputs, the tuned-problem table, and a model step under CS336_GEMM=lt."""
+
+import pytest
+import torch
+
+from cs336_systems.ops._ext import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ref(a, b, a_t, b_t):
+    A = a.float().t() if a_t else a.float()
+    B = b.float().t() if b_t else b.float()
+    return A @ B
+
+
+@pytest.mark.parametrize("a_t,b_t", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 136, 72), (1600, 480, 1024)])
+def test_lt_gemm_matches_fp32(a_t, b_t, out_dtype, M, N, K):
+    torch.manual_seed(0)
+    a = torch.randn((K, M) if a_t else (M, K), device=DEV).bfloat16()
+    b = torch.randn((N, K) if b_t else (K, N), device=DEV).bfloat16()
+    out = ops().lt_gemm(a, b, a_t, b_t, out_dtype)
+    assert out.dtype == out_dtype and out.shape == (M, N)
+    ref = _ref(a, b, a_t, b_t)
+    tol = 1e-3 if out_dtype == torch.float32 else 1e-2
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())
+
+
+def test_lt_gemm_strided_out_and_operands():
+    torch.manual_seed(1)
+    M, N, K = 192, 160, 256
+    big_a = torch.randn(K, M + 64, device=DEV).bfloat16()
+    a = big_a[:, :M]  # row stride M + 64
+    b = torch.randn(K, N, device=DEV).bfloat16()
+    bucket = torch.full((M, N + 32), 7.0, device=DEV)
+    out = bucket[:, 16:16 + N]  # a view into a larger buffer, like a DDP bucket slot
+    ops().lt_gemm_out(a, b, True, False, out)
+    torch.testing.assert_close(out, _ref(a, b, True, False), rtol=1e-3, atol=1e-2)
+    assert torch.all(bucket[:, :16] == 7.0) and torch.all(bucket[:, 16 + N:] == 7.0)
+
+
+def test_lt_gemm_table_records_tuned_problems():
+    a = torch.randn(512, 256, device=DEV).bfloat16()
+    b = torch.randn(512, 128, device=DEV).bfloat16()
+    ops().lt_gemm(a, b, True, False, torch.float32)
+    tab = list(ops().lt_gemm_table())
+    rows = [tab[i:i + 10] for i in range(0, len(tab), 10)]
+    hit = [r for r in rows if r[:6] == [256, 128, 512, 1, 0, 0]]
+    assert hit and hit[0][6] >= 1 and 0 <= hit[0][7] < hit[0][6] and hit[0][8] > 0
+
+
+def test_lt_gemm_shape_checks():
+    a = torch.randn(64, 32, device=DEV).bfloat16()
+    with pytest.raises(RuntimeError):
+        ops().lt_gemm(a, torch.randn(48, 16, device=DEV).bfloat16(), False, False, torch.float32)
+    with pytest.raises(RuntimeError):
+        ops().lt_gemm(a.float(), torch.randn(32, 16, device=DEV), False, False, torch.float32)
+
+
+def test_model_step_with_lt_gemm_matches_blas(monkeypatch):
+    from cs336_systems import ops as cops
+    from cs336_systems.models import BasicsTransformerLM
+    from cs336_systems.ops import gemm
+
+    torch.manual_seed(0)
+    model = BasicsTransformerLM(vocab_size=512, context_length=128, d_model=256, num_layers=2, num_heads=4, d_ff=1024, device=DEV)
+    x = torch.randint(0, 512, (4, 128), device=DEV)
+    y = torch.randint(0, 512, (4, 128), device=DEV)
+
+    def run():
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = model(x)
+            loss = cops.cross_entropy(logits, y)
+        loss.backward()
+        return logits.float(), {n: p.grad.clone() for n, p in model.named_parameters()}
+
+    monkeypatch.setenv("CS336_GEMM", "blas")
+    l_ref, g_ref = run()
+    monkeypatch.setenv("CS336_GEMM", "lt")
+    assert gemm.lt_gemm_enabled()
+    calls = []
+    real = ops()
+
+    class Spy:
+        def __getattr__(self, name):
+            fn = getattr(real, name)
+            if name.startswith("lt_gemm"):
+                return lambda *a: (calls.append(name), fn(*a))[1]
+            return fn
+
+    monkeypatch.setattr(gemm, "ops", lambda: Spy())
+    l_lt, g_lt = run()
+    assert "lt_gemm" in calls and "lt_gemm_out" in calls or calls.count("lt_gemm") >= 3
+    torch.testing.assert_close(l_lt, l_ref, rtol=2e-2, atol=2e-2)
+    for n in g_ref:
+        scale = g_ref[n].abs().max().item() + 1e-6
+        torch.testing.assert_close(g_lt[n] / scale, g_ref[n] / scale, rtol=0, atol=2e-2, msg=n)
