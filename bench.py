@@ -50,7 +50,12 @@ def parse(argv=None):
     # 16 -> 53.3k, 24 -> 59.2k, 32 -> 55.7k tok/s on 1 GPU; scripts/gemm_bench.py explains why)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("CS336_BENCH_BATCH", 24)), help="per-GPU batch")
     ap.add_argument("--vocab", type=int, default=10000)
-    ap.add_argument("--ddp", default="bucketed", choices=["bucketed", "individual", "flat", "naive"])
+    ap.add_argument(
+        "--ddp",
+        default="bucketed",
+        choices=["bucketed", "individual", "flat", "naive", "zero"],
+        help="zero = ZeRO-2: reduce-scattered grads, sharded fused AdamW, param all-gather under the next forward",
+    )
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--sharded", action="store_true", help="ZeRO-1 sharded optimizer state")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -113,13 +118,14 @@ def main(argv=None):
     from cs336_systems import ops
     from cs336_systems.data import synthetic_batch
     from cs336_systems.models import build_model, get_model_config, param_count, train_flops_per_token
-    from cs336_systems.parallel import DEFAULT_BUCKET_MB, ShardedOptimizer, setup_distributed, wrap_ddp
+    from cs336_systems.parallel import DEFAULT_BUCKET_MB, ShardedOptimizer, ZeroDDP, setup_distributed, wrap_ddp
 
     ops.set_backend(args.backend)
-    if world > 1:
+    zero = args.ddp == "zero"
+    if world > 1 or zero:  # (zero at world 1: a one-rank group, to measure its overhead)
         # CS336_DIST_BACKEND=gloo: rehearse the multi-rank path with several ranks on one GPU
         rank, world, device = setup_distributed(
-            backend=os.environ.get("CS336_DIST_BACKEND", "nccl"), use_gpu=torch.cuda.is_available()
+            backend=os.environ.get("CS336_DIST_BACKEND") or None, use_gpu=torch.cuda.is_available()
         )
     else:
         device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
@@ -137,19 +143,24 @@ def main(argv=None):
     n_params = sum(p.numel() for p in model.parameters())
     log(f"built {args.model}: {n_params / 1e9:.3f} B params in {time.time() - t0:.1f}s on {device}")
 
-    if world > 1:
-        bucket = args.bucket_mb if args.bucket_mb is not None else DEFAULT_BUCKET_MB
-        ddp_model = wrap_ddp(model, args.ddp, bucket_size_mb=bucket)
-    else:
-        ddp_model = model
     amp = args.dtype == "bf16" and device.type == "cuda"
     okw = dict(lr=args.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01)
     # bf16 compute-weight shadows written by the AdamW kernel (models/fused.py)
     shadows = amp and not args.no_shadows
+    bucket = args.bucket_mb if args.bucket_mb is not None else DEFAULT_BUCKET_MB
+    if zero:
+        ddp_model = ZeroDDP(model, bucket_size_mb=bucket, bf16_shadows=shadows, **okw)
+    elif world > 1:
+        ddp_model = wrap_ddp(model, args.ddp, bucket_size_mb=bucket)
+    else:
+        ddp_model = model
     overlap = args.overlap_opt == "on" or (
         args.overlap_opt == "auto" and device.type == "cuda" and args.clip == 0 and not args.sharded
     )
-    if args.sharded and world > 1:
+    if zero:
+        opt = ddp_model.optimizer
+        overlap = False
+    elif args.sharded and world > 1:
         opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw)
         overlap = False
     else:
@@ -187,9 +198,11 @@ def main(argv=None):
             logits = ddp_model(x)
             loss = ops.cross_entropy(logits, y)
         loss.backward()
-        if world > 1:
+        if world > 1 or zero:
             ddp_model.finish_gradient_synchronization()
-        if args.clip > 0:
+        if args.clip > 0 and zero:
+            ddp_model.clip_grad_norm_(args.clip)
+        elif args.clip > 0:
             ops.clip_grad_norm_(model.parameters(), args.clip)
         opt.step()
         return loss
@@ -243,14 +256,16 @@ def main(argv=None):
         "dtype": "bf16" if amp else "fp32",
         "data": "synthetic (random tokens on device, random-init weights)",
         "config": {
-            "model": f"{args.model} (GPT-2-XL shape: d_model {cfg['d_model']}, {cfg['num_layers']} layers, {cfg['num_heads']} heads, d_ff {cfg['d_ff']}, vocab {args.vocab}, {param_count(args.model, args.vocab) / 1e9:.2f}B params)",
+            "model": f"{args.model} ({'GPT-2-XL shape: ' if args.model == 'xl' else ''}d_model {cfg['d_model']}, {cfg['num_layers']} layers, {cfg['num_heads']} heads, d_ff {cfg['d_ff']}, vocab {args.vocab}, {param_count(args.model, args.vocab) / 1e9:.2f}B params)",
             "global_batch": args.batch * world,
             "per_gpu_batch": args.batch,
             "seq_len": args.ctx,
-            "parallelism": f"dp{world}" + ("+zero1" if args.sharded and world > 1 else ""),
-            "ddp": args.ddp if world > 1 else "none",
-            "bucket_mb": (args.bucket_mb if args.bucket_mb is not None else DEFAULT_BUCKET_MB) if world > 1 else None,
-            "optimizer": "fused HIP AdamW (fp32 master weights)" + (", overlapped with backward" if overlap else ""),
+            "parallelism": f"dp{world}" + ("+zero2" if zero else "+zero1" if args.sharded and world > 1 else ""),
+            "ddp": args.ddp if world > 1 or zero else "none",
+            "bucket_mb": bucket if world > 1 or zero else None,
+            "optimizer": "fused HIP AdamW (fp32 master weights)"
+            + (", overlapped with backward" if overlap else "")
+            + (", sharded 1/W with param all-gather under the forward" if zero else ""),
             "attention": "HIP FlashAttention-2 (causal)",
             "hip_graph": graphed is not None,
         },
@@ -270,7 +285,7 @@ def main(argv=None):
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     return 0

@@ -18,6 +18,7 @@ from .context_parallel import (
 )
 from .ddp import DDP, DDP_Bucketed, DDPBucketed, DDPIndividual, DEFAULT_BUCKET_MB, FlatDDP, NaiveDDP
 from .sharded_optimizer import ShardedOptimizer, ShardedStateOptimizer
+from .zero import ZeroDDP
 
 DDP_VARIANTS = {
     "naive": NaiveDDP,
@@ -61,4 +62,5 @@ __all__ = [
     "spawn",
     "supports_avg",
     "wrap_ddp",
+    "ZeroDDP",
 ]

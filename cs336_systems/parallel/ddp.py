@@ -47,6 +47,37 @@ def _unique_params(module: nn.Module) -> list[nn.Parameter]:
     return list(module.parameters())  # parameters() already de-duplicates tied weights
 
 
+def bucket_params(params: list[nn.Parameter], cap_bytes: float) -> list[list[nn.Parameter]]:
+    """Greedy buckets over ``reversed(params)`` (≈ backward order) of at most ``cap_bytes``, never
+    mixing dtypes/devices. Parameters that share one storage (the fused QKV / W1|W3 layout of
+    models/fused.py) form an indivisible unit laid out in storage order, so the grouped dW GEMM can
+    write all of them into one contiguous region of the bucket."""
+    by_storage: dict[int, list[nn.Parameter]] = {}
+    for p in params:
+        by_storage.setdefault(p.untyped_storage().data_ptr(), []).append(p)
+    units, seen = [], set()
+    for p in reversed(params):
+        key = p.untyped_storage().data_ptr()
+        if key in seen:
+            continue
+        seen.add(key)
+        units.append(sorted(by_storage[key], key=lambda t: t.storage_offset()))
+    groups: list[list[nn.Parameter]] = []
+    cur: list[nn.Parameter] = []
+    cur_bytes = 0
+    for unit in units:
+        nbytes = sum(p.numel() * p.element_size() for p in unit)
+        p = unit[0]
+        if cur and (cur_bytes + nbytes > cap_bytes or p.dtype != cur[0].dtype or p.device != cur[0].device):
+            groups.append(cur)
+            cur, cur_bytes = [], 0
+        cur.extend(unit)
+        cur_bytes += nbytes
+    if cur:
+        groups.append(cur)
+    return groups
+
+
 class _DDPBase(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, broadcast: bool = True):
         super().__init__()
@@ -188,32 +219,7 @@ class DDPBucketed(_DDPBase):
         self.bucket_size_mb = bucket_size_mb
         cap = float("inf") if bucket_size_mb is None else bucket_size_mb * 1024 * 1024
         params = [p for p in _unique_params(module) if p.requires_grad]
-        # parameters that share one storage (the fused QKV / W1|W3 layout of models/fused.py) form
-        # an indivisible unit laid out in storage order, so the grouped dW GEMM can write all of
-        # them into one contiguous region of the bucket
-        by_storage: dict[int, list[nn.Parameter]] = {}
-        for p in params:
-            by_storage.setdefault(p.untyped_storage().data_ptr(), []).append(p)
-        units, seen = [], set()
-        for p in reversed(params):
-            key = p.untyped_storage().data_ptr()
-            if key in seen:
-                continue
-            seen.add(key)
-            units.append(sorted(by_storage[key], key=lambda t: t.storage_offset()))
-        groups: list[list[nn.Parameter]] = []
-        cur: list[nn.Parameter] = []
-        cur_bytes = 0
-        for unit in units:
-            nbytes = sum(p.numel() * p.element_size() for p in unit)
-            p = unit[0]
-            if cur and (cur_bytes + nbytes > cap or p.dtype != cur[0].dtype or p.device != cur[0].device):
-                groups.append(cur)
-                cur, cur_bytes = [], 0
-            cur.extend(unit)
-            cur_bytes += nbytes
-        if cur:
-            groups.append(cur)
+        groups = bucket_params(params, cap)
         self.buckets: list[_Bucket] = []
         self._param_bucket: dict[nn.Parameter, _Bucket] = {}
         self._views: dict[nn.Parameter, torch.Tensor] = {}
