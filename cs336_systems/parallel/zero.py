@@ -92,11 +92,14 @@ class ZeroDDP(nn.Module):
         weight_decay: float = 0.01,
         bf16_shadows: bool = False,
         overlap_param_gather: bool = True,
+        _collectives_at_world1: bool = False,
     ):
         super().__init__()
         self.module = module
         self.process_group = process_group
         self.world_size = dist.get_world_size(process_group)
+        # tests: run the reduce-scatter / in-place all-gather path on a one-rank RCCL group too
+        self._solo = self.world_size == 1 and not _collectives_at_world1
         self.rank = dist.get_rank(process_group)
         self._avg = supports_avg(process_group)
         self._gloo = dist.get_backend(process_group) == "gloo"
@@ -134,9 +137,9 @@ class ZeroDDP(nn.Module):
                 master = nn.Parameter(pbuf[r * shard : (r + 1) * shard])
                 # one rank: the "shard" is the whole bucket, no collective runs and the update
                 # kernel writes the bf16 shadows itself (as FusedAdamW does without ZeRO)
-                gshard = gbuf if W == 1 else torch.zeros(shard, device=dev, dtype=torch.float32)
+                gshard = gbuf if self._solo else torch.zeros(shard, device=dev, dtype=torch.float32)
                 master.grad = gshard
-                if W == 1 and sbuf is not None:
+                if self._solo and sbuf is not None:
                     setattr(master, _SHADOW, sbuf)
                 b = _ZBucket(i, ps, pbuf, gbuf, sbuf, shard, gshard, master, self._gloo and dev.type == "cuda")
                 self.buckets.append(b)
@@ -190,7 +193,7 @@ class ZeroDDP(nn.Module):
 
     def _launch_rs(self, b: _ZBucket) -> None:
         b.launched = True
-        if self.world_size == 1:
+        if self._solo:
             return
         op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
         sync_dw_stream()
@@ -236,7 +239,7 @@ class ZeroDDP(nn.Module):
 
     # ---- parameters -------------------------------------------------------------------------
     def _launch_all_gathers(self) -> None:
-        if self.world_size == 1:  # the update wrote the parameters and their shadows in place
+        if self._solo:  # the update wrote the parameters and their shadows in place
             for b in self.buckets:
                 for p in b.params:
                     if b.sbuf is not None and p.dim() == 2:

@@ -39,10 +39,12 @@ def _lm():
                                device=DEV, fused_layout=True)
 
 
-def test_zero_world1_matches_fused_adamw(rccl_world1):
+@pytest.mark.parametrize("collectives", [False, True])
+def test_zero_world1_matches_fused_adamw(rccl_world1, collectives):
+    """collectives=True also runs the RCCL reduce-scatter and the in-place all-gather + shadow cast."""
     ref = _lm()
     ref_opt = ops.FusedAdamW(ref.parameters(), bf16_shadows=True, **OPT)
-    zero = ZeroDDP(_lm(), bucket_size_mb=2.0, bf16_shadows=True, **OPT)
+    zero = ZeroDDP(_lm(), bucket_size_mb=2.0, bf16_shadows=True, _collectives_at_world1=collectives, **OPT)
     assert len(zero.buckets) > 2
     opt = zero.optimizer
     for it in range(3):
