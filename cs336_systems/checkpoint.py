@@ -59,7 +59,7 @@ def save_checkpoint(ckpt_dir: str, step: int, model: nn.Module, optimizer: torch
     if rank == 0:
         os.makedirs(path, exist_ok=True)
     _barrier()
-    sharded = isinstance(optimizer, ShardedOptimizer) and world > 1
+    sharded = _is_sharded(optimizer) and world > 1
     if rank == 0:
         _atomic_save(_unwrap(model).state_dict(), os.path.join(path, "model.pt"))
     if optimizer is not None:
@@ -84,6 +84,11 @@ def save_checkpoint(ckpt_dir: str, step: int, model: nn.Module, optimizer: torch
     return path
 
 
+def _is_sharded(optimizer) -> bool:
+    """Per-rank optimizer state: ZeRO-1 (ShardedOptimizer) or ZeRO-2 (``ZeroDDP.optimizer``)."""
+    return isinstance(optimizer, ShardedOptimizer) or getattr(optimizer, "sharded_state", False)
+
+
 def latest_checkpoint(ckpt_dir: str) -> str | None:
     p = os.path.join(ckpt_dir, "latest")
     if not os.path.exists(p):
@@ -97,21 +102,30 @@ def latest_checkpoint(ckpt_dir: str) -> str | None:
 def load_checkpoint(path: str, model: nn.Module, optimizer: torch.optim.Optimizer | None = None, map_location="cpu") -> dict:
     """Load into ``model`` (and ``optimizer``); returns ``meta`` (``meta['step']`` = the step the
     checkpoint was taken after). A sharded checkpoint must be loaded at the same world size."""
-    rank, world = _rank_world()
     with open(os.path.join(path, "meta.json")) as f:
         meta = json.load(f)
     sd = torch.load(os.path.join(path, "model.pt"), map_location=map_location, weights_only=True)
     _unwrap(model).load_state_dict(sd)
     if optimizer is not None:
-        if meta["sharded_optimizer"]:
-            if meta["world_size"] != world:
-                raise ValueError(f"sharded optimizer checkpoint was written by {meta['world_size']} ranks, loading on {world}")
-            osd = torch.load(os.path.join(path, f"optim_rank{rank}.pt"), map_location=map_location, weights_only=True)
-        else:
-            osd = torch.load(os.path.join(path, "optim.pt"), map_location=map_location, weights_only=True)
-        optimizer.load_state_dict(osd)
-        _state_to_param_device(optimizer)
+        load_optimizer_state(path, optimizer, map_location, meta)
     return meta
+
+
+def load_optimizer_state(path: str, optimizer: torch.optim.Optimizer, map_location="cpu", meta: dict | None = None) -> None:
+    """The optimizer half of :func:`load_checkpoint` (ZeRO-2 builds its optimizer only after the
+    model weights are loaded and re-homed into its buckets)."""
+    rank, world = _rank_world()
+    if meta is None:
+        with open(os.path.join(path, "meta.json")) as f:
+            meta = json.load(f)
+    if meta["sharded_optimizer"]:
+        if meta["world_size"] != world:
+            raise ValueError(f"sharded optimizer checkpoint was written by {meta['world_size']} ranks, loading on {world}")
+        osd = torch.load(os.path.join(path, f"optim_rank{rank}.pt"), map_location=map_location, weights_only=True)
+    else:
+        osd = torch.load(os.path.join(path, "optim.pt"), map_location=map_location, weights_only=True)
+    optimizer.load_state_dict(osd)
+    _state_to_param_device(optimizer)
 
 
 def _state_to_param_device(optimizer: torch.optim.Optimizer) -> None:

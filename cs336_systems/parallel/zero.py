@@ -56,6 +56,8 @@ class _ZeroAdamW(FusedAdamW):
     """FusedAdamW over the rank's flat shards; ``step`` also launches the param all-gathers and
     ``zero_grad`` resets the model's bucket gradients (the shard gradients stay attached)."""
 
+    sharded_state = True  # one state file per rank in checkpoints (cs336_systems/checkpoint.py)
+
     def __init__(self, zero: "ZeroDDP", masters, **kw):
         super().__init__(masters, bf16_shadows=False, **kw)
         self._zero = zero
@@ -283,6 +285,11 @@ class ZeroDDP(nn.Module):
         for p in b.params:
             if p.dim() == 2:
                 mark_shadow_synced(p)
+
+    def wait_for_params(self) -> None:
+        """Make the current stream wait for every pending parameter all-gather (before reading the
+        full parameters outside a forward, e.g. for a checkpoint)."""
+        self._wait_all_gathers()
 
     def state_dict(self, *args, **kwargs):
         self._wait_all_gathers()

@@ -6,7 +6,9 @@ This driver is one torchrun-compatible entry point over the framework's pieces:
 
 * model: :func:`cs336_systems.models.build_model` (registry size or explicit dims), bf16 autocast
   over fp32 master weights, HIP kernels on GPU;
-* data parallelism: any of the four DP variants (``--ddp``) and optional ZeRO-1 (``--sharded``);
+* data parallelism: any of the four DP variants (``--ddp``) and optional ZeRO-1 (``--sharded``),
+  or ZeRO-2 (``--ddp zero``: reduce-scattered gradients, sharded fused AdamW, parameter
+  all-gather under the next forward; ``parallel/zero.py``);
 * context parallelism (``--context-parallel``, ``--cp-layout zigzag|contiguous``): each sequence is
   split over the ranks and attention runs as ring attention (``parallel/context_parallel.py``);
   the DP wrapper still averages the (replicated) weights' gradients;
@@ -44,12 +46,13 @@ import torch
 import torch.distributed as dist
 
 from . import ops
-from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
+from .checkpoint import latest_checkpoint, load_checkpoint, load_optimizer_state, save_checkpoint
 from .models import build_model
 from .models.fused import refresh_bf16_shadows
 from .parallel import (
     DEFAULT_BUCKET_MB,
     ShardedOptimizer,
+    ZeroDDP,
     cleanup_distributed,
     enable_context_parallel,
     setup_distributed,
@@ -148,24 +151,32 @@ def train(cfg: TrainConfig) -> dict:
         enable_context_parallel(model, None, cfg.cp_layout)
     okw = dict(lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.eps, weight_decay=cfg.wd)
     shadows = dev.type == "cuda" and cfg.dtype == "bf16"
-    if cfg.sharded:
+    zero = cfg.ddp == "zero"  # ZeRO-2: the wrapper owns the (sharded) optimizer, built after loading
+    if zero:
+        opt = None
+    elif cfg.sharded:
         opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw)
     else:
         opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)
 
     start = 0
-    if cfg.resume and cfg.ckpt_dir:
-        path = latest_checkpoint(cfg.ckpt_dir)
-        if path is not None:
-            meta = load_checkpoint(path, model, opt, map_location=dev)
-            start = int(meta["step"])
-            refresh_bf16_shadows(model.parameters())
-            if rank == 0:
-                print(f"resumed from {path} at step {start}", flush=True)
+    path = latest_checkpoint(cfg.ckpt_dir) if cfg.resume and cfg.ckpt_dir else None
+    if path is not None:
+        meta = load_checkpoint(path, model, opt, map_location=dev)
+        start = int(meta["step"])
+        refresh_bf16_shadows(model.parameters())
+        if rank == 0:
+            print(f"resumed from {path} at step {start}", flush=True)
     # DDP wraps after loading so its initial broadcast ships the restored weights. A HIP-graph run
     # (single process) trains the bare model: the captured backward has no collectives to issue.
-    use_graphs = cfg.graphs and world == 1 and dev.type == "cuda"
-    ddp = model if use_graphs else wrap_ddp(model, cfg.ddp, bucket_size_mb=cfg.bucket_mb)
+    use_graphs = cfg.graphs and world == 1 and dev.type == "cuda" and not zero
+    if zero:
+        ddp = ZeroDDP(model, bucket_size_mb=cfg.bucket_mb, bf16_shadows=shadows, **okw)
+        opt = ddp.optimizer
+        if path is not None:
+            load_optimizer_state(path, opt, map_location=dev)
+    else:
+        ddp = model if use_graphs else wrap_ddp(model, cfg.ddp, bucket_size_mb=cfg.bucket_mb)
     graphed = None
     batches = Batches(cfg, rank, world, dev)
     amp = dev.type == "cuda" and cfg.dtype == "bf16"
@@ -191,7 +202,7 @@ def train(cfg: TrainConfig) -> dict:
                 graphed = GraphedStep(loss_fn, model.parameters(), x, y)
             loss = graphed(x, y)  # gradients land in the graph's static tensors, re-attached to .grad
         else:
-            if hasattr(ddp, "zero_grad") and cfg.ddp in ("bucketed", "flat"):
+            if hasattr(ddp, "zero_grad") and cfg.ddp in ("bucketed", "flat", "zero"):
                 ddp.zero_grad()
             else:
                 opt.zero_grad(set_to_none=True)
@@ -199,7 +210,10 @@ def train(cfg: TrainConfig) -> dict:
                 loss = ops.cross_entropy(ddp(x), y)
             loss.backward()
             ddp.finish_gradient_synchronization()
-        gnorm = ops.clip_grad_norm_(model.parameters(), cfg.clip) if cfg.clip > 0 else None
+        if cfg.clip > 0:
+            gnorm = ddp.clip_grad_norm_(cfg.clip) if zero else ops.clip_grad_norm_(model.parameters(), cfg.clip)
+        else:
+            gnorm = None
         opt.step()
         tok_since += cfg.batch * cfg.ctx
         done = step + 1
@@ -223,6 +237,8 @@ def train(cfg: TrainConfig) -> dict:
                     log.write(json.dumps(rec) + "\n")
                     log.flush()
         if cfg.ckpt_dir and ((cfg.ckpt_every and done % cfg.ckpt_every == 0) or done == end):
+            if zero:
+                ddp.wait_for_params()  # the parameter all-gathers of this step must land first
             save_checkpoint(cfg.ckpt_dir, done, model, opt, meta=dict(config=dataclasses.asdict(cfg)))
     if log:
         log.close()

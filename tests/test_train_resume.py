@@ -1,6 +1,6 @@
 """Training driver + checkpoint/resume on CPU/gloo (world 2): a run interrupted after 3 of 6 steps
 and resumed from its checkpoint ends bit-identical to the uninterrupted run, for replicated and
-ZeRO-1-sharded optimizer state, and with a memory-mapped token file."""
+ZeRO-1-sharded optimizer state, ZeRO-2 (reduce-scatter + sharded AdamW + param all-gather), and with a memory-mapped token file."""
 
 import os
 
@@ -32,13 +32,13 @@ def _final(ckpt_dir):
     return torch.load(os.path.join(path, "model.pt"), weights_only=True)
 
 
-@pytest.mark.parametrize("sharded", [False, True])
-def test_resume_matches_uninterrupted(tmp_path, sharded):
+@pytest.mark.parametrize("sharded,ddp", [(False, "bucketed"), (True, "bucketed"), (False, "zero")])
+def test_resume_matches_uninterrupted(tmp_path, sharded, ddp):
     tokens = np.random.default_rng(0).integers(0, 500, size=20_000, dtype=np.uint16)
     data = str(tmp_path / "tokens.bin")
     tokens.tofile(data)
     common = dict(size="tiny", ctx=32, vocab=500, batch=4, steps=6, warmup=2, lr=1e-2, min_lr=1e-3, clip=1.0,
-                  ddp="bucketed", bucket_mb=0.05, sharded=sharded, data=data, device="cpu", log_every=1)
+                  ddp=ddp, bucket_mb=0.05, sharded=sharded, data=data, device="cpu", log_every=1)
     full = TrainConfig(ckpt_dir=str(tmp_path / "full"), **common)
     first = TrainConfig(ckpt_dir=str(tmp_path / "split"), stop_after=3, **common)
     second = TrainConfig(ckpt_dir=str(tmp_path / "split"), resume=True, **common)
@@ -48,7 +48,8 @@ def test_resume_matches_uninterrupted(tmp_path, sharded):
     for k in a:
         torch.testing.assert_close(a[k], b[k], rtol=0, atol=0, msg=k)
     files = sorted(os.listdir(latest_checkpoint(second.ckpt_dir)))
-    assert ("optim_rank0.pt" in files and "optim_rank1.pt" in files) if sharded else ("optim.pt" in files)
+    per_rank = sharded or ddp == "zero"
+    assert ("optim_rank0.pt" in files and "optim_rank1.pt" in files) if per_rank else ("optim.pt" in files)
 
 
 def test_parse_cli():
