@@ -237,7 +237,7 @@ class CausalMultiHeadSelfAttention(nn.Module):
     def _context_parallel_forward(self, x3, token_positions, B, N):
         """Ring attention over the context-parallel group (``parallel/context_parallel.py``): x3 is
         this rank's part of the sequence; RoPE uses the tokens' global positions."""
-        from ..parallel.context_parallel import _world_rank, ring_attention, sequence_positions
+        from ..parallel.context_parallel import _world_rank, ring_attention, sequence_positions, ulysses_attention
 
         group, layout = self.context_parallel
         H, dk = self.num_heads, self.d_k
@@ -253,6 +253,9 @@ class CausalMultiHeadSelfAttention(nn.Module):
         with annotate("rope"):
             q = self.positional_encoder(q, pos)
             k = self.positional_encoder(k, pos)
+        if layout == "ulysses":
+            with annotate("ulysses_attention"):
+                return ulysses_attention(q, k.to(q.dtype), v.to(q.dtype), group, True)
         with annotate("ring_attention"):
             return ring_attention(q, k.to(q.dtype), v.to(q.dtype), group, True, layout)
 

@@ -14,6 +14,7 @@ from .context_parallel import (
     ring_attention,
     sequence_positions,
     shard_sequence,
+    ulysses_attention,
     unshard_sequence,
 )
 from .ddp import DDP, DDP_Bucketed, DDPBucketed, DDPIndividual, DEFAULT_BUCKET_MB, FlatDDP, NaiveDDP
@@ -50,6 +51,7 @@ __all__ = [
     "sequence_positions",
     "shard_sequence",
     "unshard_sequence",
+    "ulysses_attention",
     "FlatDDP",
     "NaiveDDP",
     "ShardedOptimizer",

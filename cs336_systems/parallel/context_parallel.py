@@ -23,6 +23,13 @@ sub-chunks and gives rank r sub-chunks r and 2W−1−r, so every rank does the 
 (query sub-chunk i, key sub-chunk j) pair is full attention when j < i, causal when j == i and
 skipped when j > i.
 
+**Ulysses** (``layout="ulysses"``, DeepSpeed-Ulysses style) is the all-to-all alternative: tokens
+are sharded contiguously, and around attention two all-to-alls switch the sharding from sequence to
+heads and back — each rank attends H/W heads over the FULL sequence with one ordinary causal FA2
+call (balanced by construction), so the communication is 2 x 3 (q, k, v) + 2 (o) all-to-alls of
+n·H·D elements per layer, independent of W hops, at the price of H % W == 0. XL's 25 heads do not
+divide by 2/4/8; the 2.7b model's 32 do.
+
 Use: :func:`enable_context_parallel` on a :class:`~cs336_systems.models.BasicsTransformerLM`,
 feed each rank ``shard_sequence(tokens, rank, world, layout)`` (RoPE positions default to the
 tokens' global positions), and average gradients over the group (any DP wrapper on the same group:
@@ -40,7 +47,7 @@ import torch.nn as nn
 from ..ops._ext import use_hip
 from ..ops.flash_attention import _tiled_backward, _tiled_forward, flash_attn_bwd, flash_attn_fwd
 
-LAYOUTS = ("contiguous", "zigzag")
+LAYOUTS = ("contiguous", "zigzag", "ulysses")
 
 
 def _world_rank(group) -> tuple[int, int]:
@@ -51,7 +58,7 @@ def _world_rank(group) -> tuple[int, int]:
 
 def _sub_ids(rank: int, world: int, layout: str) -> list[int]:
     """Global sub-chunk indices held by ``rank`` (in local order)."""
-    if layout == "contiguous":
+    if layout in ("contiguous", "ulysses"):
         return [rank]
     if layout == "zigzag":
         return [rank, 2 * world - 1 - rank]
@@ -59,7 +66,7 @@ def _sub_ids(rank: int, world: int, layout: str) -> list[int]:
 
 
 def _n_sub(layout: str) -> int:
-    return 1 if layout == "contiguous" else 2
+    return 2 if layout == "zigzag" else 1
 
 
 def shard_sequence(x: torch.Tensor, rank: int, world: int, layout: str = "zigzag", dim: int = 1) -> torch.Tensor:
@@ -235,8 +242,77 @@ def ring_attention(q, k, v, group=None, causal: bool = True, layout: str = "zigz
     return RingAttention.apply(q, k, v, group, causal, layout)
 
 
+# ------------------------------------------------------------------------------------------
+# Ulysses: all-to-all between sequence sharding and head sharding
+# ------------------------------------------------------------------------------------------
+def _all_to_all(x: torch.Tensor, group) -> torch.Tensor:
+    """``all_to_all_single`` over dim 0 (W equal blocks); host-staged for gloo + GPU tensors."""
+    if x.is_cuda and dist.get_backend(group) == "gloo":
+        h = x.cpu()
+        out = torch.empty_like(h)
+        dist.all_to_all_single(out, h, group=group)
+        return out.to(x.device)
+    out = torch.empty_like(x)
+    dist.all_to_all_single(out, x, group=group)
+    return out
+
+
+def _seq_to_head(x: torch.Tensor, group) -> torch.Tensor:
+    """(B, H, n, D) with this rank's tokens -> (B, H/W, W·n, D) with this rank's heads."""
+    world, _ = _world_rank(group)
+    B, H, n, D = x.shape
+    send = x.reshape(B, world, H // world, n, D).permute(1, 0, 2, 3, 4).contiguous()  # block j -> rank j
+    recv = _all_to_all(send, group)  # block i = rank i's tokens of my heads
+    return recv.permute(1, 2, 0, 3, 4).reshape(B, H // world, world * n, D)
+
+
+def _head_to_seq(y: torch.Tensor, group) -> torch.Tensor:
+    """Inverse of :func:`_seq_to_head`."""
+    world, _ = _world_rank(group)
+    B, h, N, D = y.shape
+    n = N // world
+    send = y.reshape(B, h, world, n, D).permute(2, 0, 1, 3, 4).contiguous()  # block j = rank j's tokens
+    recv = _all_to_all(send, group)  # block i = head group i of my tokens
+    return recv.permute(1, 0, 2, 3, 4).reshape(B, world * h, n, D)
+
+
+class _SeqToHead(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return _seq_to_head(x, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _head_to_seq(g.contiguous(), ctx.group), None
+
+
+class _HeadToSeq(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, group):
+        ctx.group = group
+        return _head_to_seq(y, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _seq_to_head(g.contiguous(), ctx.group), None
+
+
+def ulysses_attention(q, k, v, group=None, causal: bool = True) -> torch.Tensor:
+    """Attention of this rank's contiguous token block (``q, k, v``: (B, H, n, D)) against the whole
+    sequence: all-to-all to head sharding, one FA2 call over the full sequence, all-to-all back."""
+    from ..ops.flash_attention import flash_attention
+
+    world, _ = _world_rank(group)
+    if q.shape[1] % world:
+        raise ValueError(f"Ulysses needs the head count ({q.shape[1]}) divisible by the group size ({world})")
+    qh, kh, vh = (_SeqToHead.apply(t, group) for t in (q, k, v))
+    return _HeadToSeq.apply(flash_attention(qh, kh, vh, causal), group)
+
+
 def enable_context_parallel(model: nn.Module, group=None, layout: str = "zigzag") -> nn.Module:
-    """Switch every attention module of ``model`` to ring attention over ``group``. The model then
+    """Switch every attention module of ``model`` to ring attention (or Ulysses all-to-all attention,
+    ``layout="ulysses"``) over ``group``. The model then
     expects each rank's :func:`shard_sequence` part of the tokens; RoPE positions default to the
     global positions of those tokens."""
     if layout not in LAYOUTS:

@@ -2,7 +2,7 @@
 (GPU tensors staged through the host), running ring attention on the HIP FA2 kernels; each rank
 checks its output and q/k/v gradients against single-call HIP attention on the full sequence.
 
-    python scripts/cp_gloo_gpu.py [--layout zigzag|contiguous]
+    python scripts/cp_gloo_gpu.py [--layout zigzag|contiguous|ulysses]
 """
 
 import argparse
@@ -18,7 +18,7 @@ sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
 
 def worker(rank, world, layout, port):
     from cs336_systems.ops.flash_attention import FlashAttentionHIP
-    from cs336_systems.parallel import ring_attention, shard_sequence
+    from cs336_systems.parallel import ring_attention, shard_sequence, ulysses_attention
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
@@ -31,13 +31,13 @@ def worker(rank, world, layout, port):
     of = FlashAttentionHIP.apply(qf.detach(), kf.detach(), vf.detach(), True)
     sh = lambda t: shard_sequence(t, rank, world, layout, dim=2)  # noqa: E731
     ql, kl, vl = (sh(t).requires_grad_(True) for t in (q, k, v))
-    o = ring_attention(ql, kl, vl, None, True, layout)
+    o = ulysses_attention(ql, kl, vl, None, True) if layout == "ulysses" else ring_attention(ql, kl, vl, None, True, layout)
     o.backward(sh(do))
     torch.testing.assert_close(o.float(), sh(of).float(), rtol=2e-2, atol=2e-2)
     for got, ref in ((ql, qf), (kl, kf), (vl, vf)):
         torch.testing.assert_close(got.grad.float(), sh(ref.grad).float(), rtol=5e-2, atol=5e-2)
     torch.cuda.synchronize()
-    print(f"rank {rank}: ring attention ({layout}, world {world}) matches full HIP FA2", flush=True)
+    print(f"rank {rank}: context-parallel attention ({layout}, world {world}) matches full HIP FA2", flush=True)
     dist.destroy_process_group()
 
 

@@ -16,6 +16,7 @@ from cs336_systems.parallel import (
     ring_attention,
     sequence_positions,
     shard_sequence,
+    ulysses_attention,
     unshard_sequence,
 )
 
@@ -52,6 +53,31 @@ def _attn_worker(rank, world, layout, causal):
 @pytest.mark.parametrize("causal", [True, False])
 def test_ring_attention_matches_full(world, layout, causal):
     spawn(_attn_worker, world, layout, causal)
+
+
+def _ulysses_worker(rank, world, causal):
+    _init(rank, world)
+    torch.manual_seed(0)
+    B, H, N, D = 2, 2 * world, 8 * world, 16
+    q, k, v, do = (torch.randn(B, H, N, D, dtype=torch.float64) for _ in range(4))
+    qf, kf, vf = (t.clone().requires_grad_(True) for t in (q, k, v))
+    naive_attention(qf, kf, vf, is_causal=causal).backward(do)
+    of = naive_attention(q, k, v, is_causal=causal)
+    sh = lambda t: shard_sequence(t, rank, world, "ulysses", dim=2)  # noqa: E731
+    ql, kl, vl = (sh(t).requires_grad_(True) for t in (q, k, v))
+    ol = ulysses_attention(ql, kl, vl, None, causal)
+    ol.backward(sh(do))
+    tol = dict(rtol=1e-10, atol=1e-10)  # the same fp64 math, only re-distributed
+    torch.testing.assert_close(ol, sh(of), **tol)
+    for got, ref in ((ql, qf), (kl, kf), (vl, vf)):
+        torch.testing.assert_close(got.grad, sh(ref.grad), **tol)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("causal", [True, False])
+def test_ulysses_attention_matches_full(world, causal):
+    spawn(_ulysses_worker, world, causal)
 
 
 def test_shard_roundtrip_and_positions():
@@ -92,6 +118,6 @@ def _model_worker(rank, world, layout):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("layout", ["contiguous", "zigzag"])
+@pytest.mark.parametrize("layout", ["contiguous", "zigzag", "ulysses"])
 def test_context_parallel_lm_matches_single_process(layout):
     spawn(_model_worker, 2, layout)

@@ -12,7 +12,7 @@ import torch.distributed as dist
 from cs336_systems import ops
 from cs336_systems.models import BasicsTransformerLM
 from cs336_systems.ops.flash_attention import FlashAttentionHIP, naive_attention
-from cs336_systems.parallel import disable_context_parallel, enable_context_parallel, ring_attention
+from cs336_systems.parallel import disable_context_parallel, enable_context_parallel, ring_attention, ulysses_attention
 from cs336_systems.parallel.comm import find_free_port
 
 pytestmark = pytest.mark.gpu
@@ -49,6 +49,21 @@ def test_ring_attention_hip_zigzag_world1(D):
         torch.testing.assert_close(got.grad.float(), r.grad, rtol=5e-2, atol=5e-2)
 
 
+def test_ulysses_world1_matches_hip_fa():
+    """World 1 over RCCL: the all-to-alls are identities, the attention is one HIP FA2 call."""
+    torch.manual_seed(1)
+    q, k, v, do = (torch.randn(2, 4, 512, 64, device=DEV, dtype=torch.bfloat16) for _ in range(4))
+    ql, kl, vl = (t.clone().requires_grad_(True) for t in (q, k, v))
+    o = ulysses_attention(ql, kl, vl, None, True)
+    o.backward(do)
+    qf, kf, vf = (t.clone().requires_grad_(True) for t in (q, k, v))
+    of = FlashAttentionHIP.apply(qf, kf, vf, True)
+    of.backward(do)
+    torch.testing.assert_close(o, of, rtol=0, atol=0)
+    for a, b in ((ql, qf), (kl, kf), (vl, vf)):
+        torch.testing.assert_close(a.grad, b.grad, rtol=0, atol=0)
+
+
 def test_context_parallel_lm_world1_matches_plain():
     torch.manual_seed(0)
     model = BasicsTransformerLM(vocab_size=512, context_length=256, d_model=256, num_layers=2, num_heads=4, d_ff=512, device=DEV)
@@ -70,7 +85,7 @@ def test_context_parallel_lm_world1_matches_plain():
         torch.testing.assert_close(g_cp[n], g_ref[n], rtol=5e-2, atol=5e-3, msg=n)
 
 
-@pytest.mark.parametrize("world,layout", [(2, "zigzag"), (4, "contiguous"), (4, "zigzag")])
+@pytest.mark.parametrize("world,layout", [(2, "zigzag"), (4, "contiguous"), (4, "zigzag"), (2, "ulysses"), (4, "ulysses")])
 def test_ring_attention_multirank_one_gpu(world, layout):
     """2-4 ranks share cuda:0 (gloo, host-staged P2P): the multi-hop ring on the HIP kernels."""
     import subprocess
