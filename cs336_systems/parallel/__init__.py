@@ -19,6 +19,7 @@ from .context_parallel import (
 )
 from .ddp import DDP, DDP_Bucketed, DDPBucketed, DDPIndividual, DEFAULT_BUCKET_MB, FlatDDP, NaiveDDP
 from .sharded_optimizer import ShardedOptimizer, ShardedStateOptimizer
+from .tensor_parallel import gather_tp_state_dict, tensor_parallel_
 from .zero import ZeroDDP
 
 DDP_VARIANTS = {
@@ -65,4 +66,6 @@ __all__ = [
     "supports_avg",
     "wrap_ddp",
     "ZeroDDP",
+    "gather_tp_state_dict",
+    "tensor_parallel_",
 ]
