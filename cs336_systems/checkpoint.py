@@ -51,17 +51,20 @@ def _atomic_save(obj, path: str) -> None:
     os.replace(tmp, path)
 
 
-def save_checkpoint(ckpt_dir: str, step: int, model: nn.Module, optimizer: torch.optim.Optimizer | None = None, meta: dict | None = None, keep: int = 2) -> str:
-    """Collective: every rank must call it. Returns the checkpoint directory."""
+def save_checkpoint(ckpt_dir: str, step: int, model: nn.Module, optimizer: torch.optim.Optimizer | None = None, meta: dict | None = None, keep: int = 2,
+                    model_state: dict | None = None, sharded: bool | None = None) -> str:
+    """Collective: every rank must call it. Returns the checkpoint directory. ``model_state``
+    overrides ``model.state_dict()`` (e.g. the gathered state of a tensor-parallel model) and
+    ``sharded=True`` writes one optimizer file per rank whatever the optimizer type."""
     rank, world = _rank_world()
     name = f"step_{step:08d}"
     path = os.path.join(ckpt_dir, name)
     if rank == 0:
         os.makedirs(path, exist_ok=True)
     _barrier()
-    sharded = _is_sharded(optimizer) and world > 1
+    sharded = (_is_sharded(optimizer) if sharded is None else sharded) and world > 1
     if rank == 0:
-        _atomic_save(_unwrap(model).state_dict(), os.path.join(path, "model.pt"))
+        _atomic_save(model_state if model_state is not None else _unwrap(model).state_dict(), os.path.join(path, "model.pt"))
     if optimizer is not None:
         if sharded:
             _atomic_save(optimizer.state_dict(), os.path.join(path, f"optim_rank{rank}.pt"))

@@ -109,6 +109,30 @@ def tensor_parallel_(model: nn.Module, group=None, broadcast: bool = True) -> nn
     return model
 
 
+@torch.no_grad()
+def tp_clip_grad_norm_(model: nn.Module, max_norm: float, group=None) -> torch.Tensor:
+    """Global gradient L2 norm of a tensor-parallel model (sharded gradients summed over the group,
+    replicated ones counted once), then scale every gradient by ``min(1, max_norm / (norm + 1e-6))``."""
+    sq_shard, sq_rep = None, None
+    for name, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        s = p.grad.float().pow(2).sum()
+        if _tp_split(name) is None:
+            sq_rep = s if sq_rep is None else sq_rep + s
+        else:
+            sq_shard = s if sq_shard is None else sq_shard + s
+    dev = next(model.parameters()).device
+    sq_shard = torch.zeros((), device=dev) if sq_shard is None else sq_shard
+    sq_rep = torch.zeros((), device=dev) if sq_rep is None else sq_rep
+    norm = (_all_reduce(sq_shard.reshape(1), group)[0] + sq_rep).sqrt()
+    scale = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+    for p in model.parameters():
+        if p.grad is not None:
+            p.grad.mul_(scale.to(p.grad.dtype))
+    return norm
+
+
 def _tp_split(name: str) -> int | None:
     """Dim along which parameter ``name`` is sharded (0 rows, 1 columns), None if replicated."""
     if name.endswith(("attn.q_proj.weight", "attn.k_proj.weight", "attn.v_proj.weight", "ffn.w1.weight", "ffn.w3.weight")):

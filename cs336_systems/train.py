@@ -9,6 +9,9 @@ This driver is one torchrun-compatible entry point over the framework's pieces:
 * data parallelism: any of the four DP variants (``--ddp``) and optional ZeRO-1 (``--sharded``),
   or ZeRO-2 (``--ddp zero``: reduce-scattered gradients, sharded fused AdamW, parameter
   all-gather under the next forward; ``parallel/zero.py``);
+* tensor parallelism (``--tensor-parallel``): heads and d_ff sharded over all ranks
+  (``parallel/tensor_parallel.py``), every rank on the whole batch, checkpoints hold the gathered
+  weights and one optimizer shard per rank;
 * context parallelism (``--context-parallel``, ``--cp-layout zigzag|contiguous``): each sequence is
   split over the ranks and attention runs as ring attention (``parallel/context_parallel.py``);
   the DP wrapper still averages the (replicated) weights' gradients;
@@ -49,10 +52,13 @@ from . import ops
 from .checkpoint import latest_checkpoint, load_checkpoint, load_optimizer_state, save_checkpoint
 from .models import build_model
 from .models.fused import refresh_bf16_shadows
+from .parallel.tensor_parallel import tp_clip_grad_norm_
 from .parallel import (
     DEFAULT_BUCKET_MB,
     ShardedOptimizer,
     ZeroDDP,
+    gather_tp_state_dict,
+    tensor_parallel_,
     cleanup_distributed,
     enable_context_parallel,
     setup_distributed,
@@ -82,6 +88,7 @@ class TrainConfig:
     sharded: bool = False
     context_parallel: bool = False  # split every sequence over the ranks (ring attention) instead of the batch
     cp_layout: str = "zigzag"
+    tensor_parallel: bool = False  # shard heads / d_ff over all ranks (Megatron-style TP) instead of the batch
     graphs: bool = False  # single process on GPU: replay fwd + loss + bwd from one captured HIP graph
     data: str | None = None  # token file; None = synthetic
     seed: int = 0
@@ -115,17 +122,18 @@ class Batches:
 
     def __init__(self, cfg: TrainConfig, rank: int, world: int, device: torch.device):
         self.cp = cfg.context_parallel and world > 1
-        if cfg.batch % world and not self.cp:
+        self.tp = cfg.tensor_parallel and world > 1  # every rank takes the whole batch
+        if cfg.batch % world and not (self.cp or self.tp):
             raise ValueError(f"global batch {cfg.batch} must divide by world size {world}")
         self.world = world
-        self.cfg, self.rank, self.local, self.device = cfg, rank, (cfg.batch if self.cp else cfg.batch // world), device
+        self.cfg, self.rank, self.local, self.device = cfg, rank, (cfg.batch if self.cp or self.tp else cfg.batch // world), device
         self.tokens = open_tokens(cfg.data) if cfg.data else None
 
     def __call__(self, step: int) -> tuple[torch.Tensor, torch.Tensor]:
         cfg = self.cfg
         g = torch.Generator().manual_seed(cfg.seed * 1_000_003 + step)
         # context parallel: every rank takes the whole batch and its part of each sequence
-        lo, hi = (0, cfg.batch) if self.cp else (self.rank * self.local, (self.rank + 1) * self.local)
+        lo, hi = (0, cfg.batch) if self.cp or self.tp else (self.rank * self.local, (self.rank + 1) * self.local)
         if self.tokens is None:
             toks = torch.randint(0, cfg.vocab, (cfg.batch, cfg.ctx + 1), generator=g)[lo:hi]
         else:
@@ -152,7 +160,8 @@ def train(cfg: TrainConfig) -> dict:
     okw = dict(lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.eps, weight_decay=cfg.wd)
     shadows = dev.type == "cuda" and cfg.dtype == "bf16"
     zero = cfg.ddp == "zero"  # ZeRO-2: the wrapper owns the (sharded) optimizer, built after loading
-    if zero:
+    tp = cfg.tensor_parallel and world > 1  # TP: shard after loading the full weights, then build the optimizer
+    if zero or tp:
         opt = None
     elif cfg.sharded:
         opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw)
@@ -170,7 +179,13 @@ def train(cfg: TrainConfig) -> dict:
     # DDP wraps after loading so its initial broadcast ships the restored weights. A HIP-graph run
     # (single process) trains the bare model: the captured backward has no collectives to issue.
     use_graphs = cfg.graphs and world == 1 and dev.type == "cuda" and not zero
-    if zero:
+    if tp:
+        tensor_parallel_(model)  # heads and d_ff over all ranks; no data-parallel wrapper
+        opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)
+        if path is not None:
+            load_optimizer_state(path, opt, map_location=dev)
+        ddp = model
+    elif zero:
         ddp = ZeroDDP(model, bucket_size_mb=cfg.bucket_mb, bf16_shadows=shadows, **okw)
         opt = ddp.optimizer
         if path is not None:
@@ -209,8 +224,11 @@ def train(cfg: TrainConfig) -> dict:
             with autocast():
                 loss = ops.cross_entropy(ddp(x), y)
             loss.backward()
-            ddp.finish_gradient_synchronization()
-        if cfg.clip > 0:
+            if not tp:
+                ddp.finish_gradient_synchronization()
+        if cfg.clip > 0 and tp:
+            gnorm = tp_clip_grad_norm_(model, cfg.clip)
+        elif cfg.clip > 0:
             gnorm = ddp.clip_grad_norm_(cfg.clip) if zero else ops.clip_grad_norm_(model.parameters(), cfg.clip)
         else:
             gnorm = None
@@ -239,7 +257,11 @@ def train(cfg: TrainConfig) -> dict:
         if cfg.ckpt_dir and ((cfg.ckpt_every and done % cfg.ckpt_every == 0) or done == end):
             if zero:
                 ddp.wait_for_params()  # the parameter all-gathers of this step must land first
-            save_checkpoint(cfg.ckpt_dir, done, model, opt, meta=dict(config=dataclasses.asdict(cfg)))
+            if tp:  # the full weights (gathered) and one optimizer file per rank
+                save_checkpoint(cfg.ckpt_dir, done, model, opt, meta=dict(config=dataclasses.asdict(cfg)),
+                                model_state=gather_tp_state_dict(model), sharded=True)
+            else:
+                save_checkpoint(cfg.ckpt_dir, done, model, opt, meta=dict(config=dataclasses.asdict(cfg)))
     if log:
         log.close()
     return dict(rank=rank, world=world, start=start, history=hist, final_loss=loss_val)

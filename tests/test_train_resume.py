@@ -1,6 +1,6 @@
 """Training driver + checkpoint/resume on CPU/gloo (world 2): a run interrupted after 3 of 6 steps
 and resumed from its checkpoint ends bit-identical to the uninterrupted run, for replicated and
-ZeRO-1-sharded optimizer state, ZeRO-2 (reduce-scatter + sharded AdamW + param all-gather), and with a memory-mapped token file."""
+ZeRO-1-sharded optimizer state, ZeRO-2 (reduce-scatter + sharded AdamW + param all-gather), tensor parallelism, and with a memory-mapped token file."""
 
 import os
 
@@ -32,13 +32,14 @@ def _final(ckpt_dir):
     return torch.load(os.path.join(path, "model.pt"), weights_only=True)
 
 
-@pytest.mark.parametrize("sharded,ddp", [(False, "bucketed"), (True, "bucketed"), (False, "zero")])
-def test_resume_matches_uninterrupted(tmp_path, sharded, ddp):
+@pytest.mark.parametrize("sharded,ddp,tp", [(False, "bucketed", False), (True, "bucketed", False), (False, "zero", False),
+                                            (False, "bucketed", True)])
+def test_resume_matches_uninterrupted(tmp_path, sharded, ddp, tp):
     tokens = np.random.default_rng(0).integers(0, 500, size=20_000, dtype=np.uint16)
     data = str(tmp_path / "tokens.bin")
     tokens.tofile(data)
     common = dict(size="tiny", ctx=32, vocab=500, batch=4, steps=6, warmup=2, lr=1e-2, min_lr=1e-3, clip=1.0,
-                  ddp=ddp, bucket_mb=0.05, sharded=sharded, data=data, device="cpu", log_every=1)
+                  ddp=ddp, bucket_mb=0.05, sharded=sharded, tensor_parallel=tp, data=data, device="cpu", log_every=1)
     full = TrainConfig(ckpt_dir=str(tmp_path / "full"), **common)
     first = TrainConfig(ckpt_dir=str(tmp_path / "split"), stop_after=3, **common)
     second = TrainConfig(ckpt_dir=str(tmp_path / "split"), resume=True, **common)
@@ -48,7 +49,7 @@ def test_resume_matches_uninterrupted(tmp_path, sharded, ddp):
     for k in a:
         torch.testing.assert_close(a[k], b[k], rtol=0, atol=0, msg=k)
     files = sorted(os.listdir(latest_checkpoint(second.ckpt_dir)))
-    per_rank = sharded or ddp == "zero"
+    per_rank = sharded or ddp == "zero" or tp
     assert ("optim_rank0.pt" in files and "optim_rank1.pt" in files) if per_rank else ("optim.pt" in files)
 
 
@@ -64,6 +65,24 @@ def _cp_worker(rank, world, cfg):
 
     train(cfg)
     dist.destroy_process_group()
+
+
+def test_tensor_parallel_training_matches_single_rank(tmp_path):
+    """2-rank tensor-parallel training (heads and d_ff split, clipping on) ends at the parameters
+    of a 1-rank run over the same batches (the checkpoint holds the gathered weights)."""
+    common = dict(size="tiny", ctx=32, vocab=500, batch=2, steps=3, warmup=1, lr=1e-3, min_lr=1e-4, clip=1.0,
+                  device="cpu", log_every=1)
+    one = TrainConfig(ckpt_dir=str(tmp_path / "one"), **common)
+    tpc = TrainConfig(ckpt_dir=str(tmp_path / "tp"), tensor_parallel=True, **common)
+    spawn(_cp_worker, 1, one)
+    spawn(_cp_worker, 2, tpc)
+    a, b = _final(one.ckpt_dir), _final(tpc.ckpt_dir)
+    assert a.keys() == b.keys()
+    for k in a:
+        diff = (a[k] - b[k]).abs()
+        # Adam moves a weight ~lr (1e-3) per step; only weights whose gradient is within rounding
+        # of zero may differ at that scale, the rest must agree far below it
+        assert diff.max() <= 6e-3 and (diff > 1e-5).float().mean() < 0.01, (k, diff.max(), (diff > 1e-5).float().mean())
 
 
 def test_context_parallel_training_matches_single_rank(tmp_path):
