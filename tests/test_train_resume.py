@@ -97,5 +97,6 @@ def test_context_parallel_training_matches_single_rank(tmp_path):
     a, b = _final(one.ckpt_dir), _final(cp.ckpt_dir)
     for k in a:
         # AdamW moves each weight by ~lr per step, so fp32 rounding differences in near-zero
-        # gradients may show up at that scale
-        torch.testing.assert_close(a[k], b[k], rtol=0, atol=2e-3 * 3, msg=k)
+        # gradients may show up at that scale — but only for a small fraction of the weights
+        diff = (a[k] - b[k]).abs()
+        assert diff.max() <= 6e-3 and (diff > 1e-5).float().mean() < 0.01, (k, diff.max(), (diff > 1e-5).float().mean())
