@@ -9,6 +9,7 @@
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
+#include <cstdlib>
 #include <vector>
 
 #include "cs336/kernels.h"
@@ -71,6 +72,12 @@ void fill_attn(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, c
   p.D = (int)q.size(3);
   p.scale = (float)scale;
   p.causal = causal;
+  // CS336_FA_ORDER=0 restores the per-head interleaved block order (A/B switch for tile_order)
+  static const int order = [] {
+    const char* e = std::getenv("CS336_FA_ORDER");
+    return e ? std::atoi(e) : 1;
+  }();
+  p.order = order;
 }
 
 using OptT = std::optional<at::Tensor>;

@@ -45,10 +45,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int l32 = lane & 31, hh = lane >> 5;
   const int nqb = (p.Nq + BM - 1) / BM;
-  const int total = nqb * p.B * p.H;
-  const int rid = xcd_remap(blockIdx.x, total);
-  const int bh = rid / nqb;
-  int qb = rid % nqb;
+  int bh, qb;
+  tile_order(blockIdx.x, p.B * p.H, nqb, CAUSAL ? p.order : 0, bh, qb);
   if (CAUSAL) qb = nqb - 1 - qb;
   const int b = bh / p.H, h = bh % p.H;
   const int q0 = qb * BM;
@@ -264,10 +262,8 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int l32 = lane & 31, hh = lane >> 5;
   const int nkb = (p.Nk + BK - 1) / BK;
-  const int total = nkb * p.B * p.H;
-  const int rid = xcd_remap(blockIdx.x, total);
-  const int bh = rid / nkb;
-  const int kb = rid % nkb;  // ascending = heaviest first under the causal mask
+  int bh, kb;  // ascending kb = heaviest first under the causal mask
+  tile_order(blockIdx.x, p.B * p.H, nkb, CAUSAL ? p.order : 0, bh, kb);
   const int b = bh / p.H, h = bh % p.H;
   const int k0 = kb * BK;
   const int kw0 = k0 + wave * 32;

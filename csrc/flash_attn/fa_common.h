@@ -257,5 +257,23 @@ __device__ __forceinline__ int xcd_remap(int bid, int total) {
   return base + (bid >> 3);
 }
 
+// (batch*head, tile level) of block `bid` for a grid of nbh*nt blocks. order 0: xcd_remap, levels of
+// one head adjacent. order 1 (causal LPT): each XCD still owns a contiguous range of heads (its L2
+// keeps their K/V), but inside the range all heads' level-0 tiles are dispatched first, then level
+// 1, ...; callers map level 0 to the heaviest tile under the causal mask, so the short tiles fill the
+// tail of the grid instead of a long one starting last. Needs nbh % 8 == 0 (bid & 7 = XCD), else
+// falls back to order 0.
+__device__ __forceinline__ void tile_order(int bid, int nbh, int nt, int order, int& bh, int& lvl) {
+  if (order == 1 && (nbh & 7) == 0) {
+    const int per = nbh >> 3, j = bid >> 3;
+    bh = (bid & 7) * per + j % per;
+    lvl = j / per;
+  } else {
+    const int rid = xcd_remap(bid, nbh * nt);
+    bh = rid / nt;
+    lvl = rid % nt;
+  }
+}
+
 }  // namespace fa
 }  // namespace cs336

@@ -39,10 +39,8 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
   const int l32 = lane & 31, hh = lane >> 5;
 
   const int nqb = (p.Nq + BM - 1) / BM;
-  const int total = nqb * p.B * p.H;
-  const int rid = xcd_remap(blockIdx.x, total);
-  const int bh = rid / nqb;
-  int qb = rid % nqb;
+  int bh, qb;
+  tile_order(blockIdx.x, p.B * p.H, nqb, CAUSAL ? p.order : 0, bh, qb);
   if (CAUSAL) qb = nqb - 1 - qb;
   const int b = bh / p.H, h = bh % p.H;
   const int q0 = qb * BM;

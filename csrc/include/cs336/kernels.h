@@ -112,6 +112,9 @@ struct AttnParams {
   const float* rope_cos = nullptr;
   const float* rope_sin = nullptr;
   const int64_t* rope_pos = nullptr;
+  // block dispatch order under the causal mask: 0 = per-(batch, head) interleaved, 1 = heaviest tile
+  // level first within each XCD's heads (longest-processing-time order, see tile_order in fa_common.h)
+  int order = 1;
 };
 
 struct AttnBwdParams {
