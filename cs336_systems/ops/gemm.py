@@ -12,6 +12,12 @@ hipBLASLt with per-problem autotuning over the heuristic's top candidates (``CS3
 default 48), fp32 output included, which TunableOp does not cover. On the XL shapes the tuned pick
 is within noise of ``torch.mm``'s on most GEMMs and 1.1-1.5x faster on a few fp32-output weight
 gradients (``profiles/r1_lt_gemm_sweep*.json``), so ``blas`` stays the default.
+
+``CS336_GEMM=best`` takes the faster of the two per problem: the first time a (kind, shapes,
+strides, output) problem is seen outside graph capture, ``torch.mm`` and the autotuned ``lt_gemm``
+are each timed on it (HIP events on the current stream) and the winner is cached for the process.
+The sweep shows why neither alone is right: ``lt`` wins 1.2x on the QKV GEMMs and the lm_head weight
+gradient but loses 1.2x on the W1|W3 weight gradient from ``Xᵀ``.
 """
 
 from __future__ import annotations
@@ -24,11 +30,55 @@ from ._ext import ext_available, ops
 
 
 def hip_gemm_enabled() -> bool:
-    return os.environ.get("CS336_GEMM", "blas").lower() == "hip" and ext_available()
+    return _mode() == "hip"
 
 
 def lt_gemm_enabled() -> bool:
-    return os.environ.get("CS336_GEMM", "blas").lower() == "lt" and ext_available()
+    """``lt`` or ``best`` (the autotuned hipBLASLt op may be used)."""
+    return _mode() in ("lt", "best")
+
+
+def _mode() -> str:
+    m = os.environ.get("CS336_GEMM", "blas").lower()
+    return m if m in ("lt", "best", "hip") and ext_available() else "blas"
+
+
+_BEST: dict = {}
+
+
+def _time_ms(fn, reps: int = 5) -> float:
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def _use_lt(kind: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None, lt_fn, blas_fn) -> bool:
+    """``lt`` mode: always; ``best`` mode: the cached per-problem winner (``torch.mm`` on ties and
+    while a HIP graph is being captured, where nothing can be timed)."""
+    mode = _mode()
+    if mode == "lt":
+        return True
+    if mode != "best":
+        return False
+    key = (kind, tuple(a.shape), a.stride(), tuple(b.shape), b.stride(),
+           None if out is None else (out.dtype, out.stride()))
+    hit = _BEST.get(key)
+    if hit is None:
+        if torch.cuda.is_current_stream_capturing():
+            return False
+        t_lt, t_blas = _time_ms(lt_fn), _time_ms(blas_fn)
+        hit = _BEST[key] = t_lt < 0.97 * t_blas
+    return hit
+
+
+def gemm_choices() -> dict:
+    """``best`` mode decisions so far: problem key -> True when ``lt_gemm`` won."""
+    return dict(_BEST)
 
 
 def _lt_ok(*ts) -> bool:
@@ -42,7 +92,9 @@ def _ok(a, b, ta, tb) -> bool:
 def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``x @ w.T`` (forward of a linear layer)."""
     if lt_gemm_enabled() and _lt_ok(x, w):
-        return ops().lt_gemm(x, w, False, True, torch.bfloat16)
+        lt = lambda: ops().lt_gemm(x, w, False, True, torch.bfloat16)  # noqa: E731
+        if _use_lt("nt", x, w, None, lt, lambda: torch.mm(x, w.t())):
+            return lt()
     if hip_gemm_enabled() and _ok(x, w, False, True):
         return ops().gemm(x, w, False, True, torch.bfloat16, 0, 0, 0)
     return torch.mm(x, w.t())
@@ -51,7 +103,9 @@ def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 def mm_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``dy @ w`` (input gradient)."""
     if lt_gemm_enabled() and _lt_ok(dy, w):
-        return ops().lt_gemm(dy, w, False, False, torch.bfloat16)
+        lt = lambda: ops().lt_gemm(dy, w, False, False, torch.bfloat16)  # noqa: E731
+        if _use_lt("nn", dy, w, None, lt, lambda: torch.mm(dy, w)):
+            return lt()
     if hip_gemm_enabled() and _ok(dy, w, False, False):
         return ops().gemm(dy, w, False, False, torch.bfloat16, 0, 0, 0)
     return torch.mm(dy, w)
@@ -62,9 +116,14 @@ def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None =
     (K_in, tokens). hipBLASLt only: its NT kernels are the fast ones for this layout."""
     if lt_gemm_enabled() and _lt_ok(dy, xt) and (out is None or out.stride(1) == 1):
         if out is None:
-            return ops().lt_gemm(dy, xt, True, True, torch.float32)
-        ops().lt_gemm_out(dy, xt, True, True, out)
-        return out
+            lt = lambda: ops().lt_gemm(dy, xt, True, True, torch.float32)  # noqa: E731
+            blas = lambda: torch.mm(dy.t(), xt.t(), out_dtype=torch.float32)  # noqa: E731
+        else:
+            lt = lambda: ops().lt_gemm_out(dy, xt, True, True, out)  # noqa: E731
+            blas = lambda: torch.mm(dy.t(), xt.t(), out_dtype=torch.float32, out=out)  # noqa: E731
+        if _use_lt("tt32", dy, xt, out, lt, blas):
+            r = lt()
+            return out if out is not None else r
     if out is not None:
         torch.mm(dy.t(), xt.t(), out_dtype=torch.float32, out=out)
         return out
@@ -75,9 +134,14 @@ def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = Non
     """``dy.T @ x`` with an fp32 result (weight gradient), written into ``out`` when given."""
     if lt_gemm_enabled() and _lt_ok(dy, x) and (out is None or out.stride(1) == 1):
         if out is None:
-            return ops().lt_gemm(dy, x, True, False, torch.float32)
-        ops().lt_gemm_out(dy, x, True, False, out)
-        return out
+            lt = lambda: ops().lt_gemm(dy, x, True, False, torch.float32)  # noqa: E731
+            blas = lambda: torch.mm(dy.t(), x, out_dtype=torch.float32)  # noqa: E731
+        else:
+            lt = lambda: ops().lt_gemm_out(dy, x, True, False, out)  # noqa: E731
+            blas = lambda: torch.mm(dy.t(), x, out_dtype=torch.float32, out=out)  # noqa: E731
+        if _use_lt("tn32", dy, x, out, lt, blas):
+            r = lt()
+            return out if out is not None else r
     if hip_gemm_enabled() and _ok(dy, x, True, False):
         if out is not None:
             ops().gemm_out(dy, x, True, False, out, False, 0, 0, 0)

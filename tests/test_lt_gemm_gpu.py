@@ -101,3 +101,33 @@ def test_model_step_with_lt_gemm_matches_blas(monkeypatch):
     for n in g_ref:
         scale = g_ref[n].abs().max().item() + 1e-6
         torch.testing.assert_close(g_lt[n] / scale, g_ref[n] / scale, rtol=0, atol=2e-2, msg=n)
+
+
+def test_best_mode_picks_per_problem_and_matches_fp32(monkeypatch):
+    """CS336_GEMM=best: every projection-GEMM entry point returns the fp32-reference result whichever
+    backend wins the timing, and the decision is cached once per problem."""
+    from cs336_systems.ops import gemm
+
+    monkeypatch.setenv("CS336_GEMM", "best")
+    gemm._BEST.clear()
+    torch.manual_seed(3)
+    T, K, N = 512, 256, 384
+    x = torch.randn(T, K, device=DEV).bfloat16()
+    w = torch.randn(N, K, device=DEV).bfloat16()
+    dy = torch.randn(T, N, device=DEV).bfloat16()
+    y = gemm.mm_nt(x, w)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), rtol=1e-2, atol=1e-2 * K**0.5 * 4)
+    dx = gemm.mm_nn(dy, w)
+    torch.testing.assert_close(dx.float(), dy.float() @ w.float(), rtol=1e-2, atol=1e-2 * N**0.5 * 4)
+    ref_dw = dy.float().t() @ x.float()
+    out = torch.zeros(N, K, device=DEV)
+    assert gemm.mm_tn_fp32(dy, x, out=out) is out
+    torch.testing.assert_close(out, ref_dw, rtol=1e-3, atol=1e-3 * ref_dw.abs().max().item())
+    xt = x.t().contiguous()
+    dw2 = gemm.mm_tn_fp32_xt(dy, xt)
+    torch.testing.assert_close(dw2, ref_dw, rtol=1e-3, atol=1e-3 * ref_dw.abs().max().item())
+    choices = gemm.gemm_choices()
+    assert {k[0] for k in choices} == {"nt", "nn", "tn32", "tt32"}
+    n = len(choices)
+    gemm.mm_nt(x, w)
+    assert len(gemm.gemm_choices()) == n  # cached, not re-timed
