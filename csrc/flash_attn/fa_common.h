@@ -258,16 +258,20 @@ __device__ __forceinline__ int xcd_remap(int bid, int total) {
 }
 
 // (batch*head, tile level) of block `bid` for a grid of nbh*nt blocks. order 0: xcd_remap, levels of
-// one head adjacent. order 1 (causal LPT): each XCD still owns a contiguous range of heads (its L2
-// keeps their K/V), but inside the range all heads' level-0 tiles are dispatched first, then level
-// 1, ...; callers map level 0 to the heaviest tile under the causal mask, so the short tiles fill the
-// tail of the grid instead of a long one starting last. Needs nbh % 8 == 0 (bid & 7 = XCD), else
-// falls back to order 0.
+// one head adjacent. order 1 (causal LPT): callers map level 0 to the heaviest tile under the causal
+// mask, and every head's level-0 tile is dispatched before any level-1 tile, ..., so the short tiles
+// fill the tail of the grid instead of a long one starting last. With nbh % 8 == 0 each XCD (bid & 7)
+// also keeps a contiguous range of heads, whose K/V then stay in its L2; otherwise the order is
+// level-major over the whole grid (order 2 forces that form; measured equal to the XCD-range form
+// when nbh % 8 == 0 and 5-8 % faster than order 0 at (3, 25, 4096, 64): profiles/r1_fa_lpt_order.md).
 __device__ __forceinline__ void tile_order(int bid, int nbh, int nt, int order, int& bh, int& lvl) {
   if (order == 1 && (nbh & 7) == 0) {
     const int per = nbh >> 3, j = bid >> 3;
     bh = (bid & 7) * per + j % per;
     lvl = j / per;
+  } else if (order != 0) {
+    bh = bid % nbh;
+    lvl = bid / nbh;
   } else {
     const int rid = xcd_remap(bid, nbh * nt);
     bh = rid / nt;

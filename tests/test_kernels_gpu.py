@@ -163,8 +163,21 @@ def _ref_attn(q, k, v, causal):
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("N", [128, 200, 512])
 def test_flash_fwd_bwd(dt, D, causal, N):
+    _check_flash(dt, D, causal, N, 2, 3)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("N", [200, 512])
+@pytest.mark.parametrize("B,H", [(2, 4), (4, 6)])
+def test_flash_fwd_bwd_xcd_head_ranges(D, causal, N, B, H):
+    """B*H % 8 == 0: the causal grid takes the per-XCD head-range LPT order of tile_order
+    (csrc/flash_attn/fa_common.h); B*H = 6 above takes the global level-major form."""
+    _check_flash(torch.bfloat16, D, causal, N, B, H)
+
+
+def _check_flash(dt, D, causal, N, B, H):
     torch.manual_seed(0)
-    B, H = 2, 3
     # (B, N, H, D) memory viewed as (B, H, N, D): the model's layout
     mk = lambda: torch.randn(B, N, H, D, device=DEV, dtype=dt).transpose(1, 2).requires_grad_(True)
     q, k, v = mk(), mk(), mk()
