@@ -9,6 +9,7 @@
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -78,6 +79,9 @@ void fill_attn(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, c
     return e ? std::atoi(e) : 1;
   }();
   p.order = order;
+  // heads whose K+V fit one XCD's 4 MB L2 form one level-major group (tile_order, fa_common.h)
+  const int64_t kv_head = 2 * (int64_t)p.Nk * p.D * (int64_t)q.element_size();
+  p.lpt_group = (int)std::max<int64_t>(1, std::min<int64_t>(1 << 20, (int64_t(4) << 20) / std::max<int64_t>(kv_head, 1)));
 }
 
 using OptT = std::optional<at::Tensor>;

@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   const int l32 = lane & 31, hh = lane >> 5;
   const int nqb = (p.Nq + BM - 1) / BM;
   int bh, qb;
-  tile_order(blockIdx.x, p.B * p.H, nqb, CAUSAL ? p.order : 0, bh, qb);
+  tile_order(blockIdx.x, p.B * p.H, nqb, CAUSAL ? p.order : 0, p.lpt_group, bh, qb);
   if (CAUSAL) qb = nqb - 1 - qb;
   const int b = bh / p.H, h = bh % p.H;
   const int q0 = qb * BM;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
   const int l32 = lane & 31, hh = lane >> 5;
   const int nkb = (p.Nk + BK - 1) / BK;
   int bh, kb;  // ascending kb = heaviest first under the causal mask
-  tile_order(blockIdx.x, p.B * p.H, nkb, CAUSAL ? p.order : 0, bh, kb);
+  tile_order(blockIdx.x, p.B * p.H, nkb, CAUSAL ? p.order : 0, p.lpt_group, bh, kb);
   const int b = bh / p.H, h = bh % p.H;
   const int k0 = kb * BK;
   const int kw0 = k0 + wave * 32;

@@ -259,19 +259,31 @@ __device__ __forceinline__ int xcd_remap(int bid, int total) {
 
 // (batch*head, tile level) of block `bid` for a grid of nbh*nt blocks. order 0: xcd_remap, levels of
 // one head adjacent. order 1 (causal LPT): callers map level 0 to the heaviest tile under the causal
-// mask, and every head's level-0 tile is dispatched before any level-1 tile, ..., so the short tiles
-// fill the tail of the grid instead of a long one starting last. With nbh % 8 == 0 each XCD (bid & 7)
-// also keeps a contiguous range of heads, whose K/V then stay in its L2; otherwise the order is
-// level-major over the whole grid (order 2 forces that form; measured equal to the XCD-range form
-// when nbh % 8 == 0 and 5-8 % faster than order 0 at (3, 25, 4096, 64): profiles/r1_fa_lpt_order.md).
-__device__ __forceinline__ void tile_order(int bid, int nbh, int nt, int order, int& bh, int& lvl) {
+// mask. Heads are taken in groups of `grp`; inside a group every head's level-0 tile is dispatched
+// before any level-1 tile, ..., so the short tiles fill the tail of the grid instead of a long one
+// starting last (the light tiles of one group run next to the heavy ones of the next). The host sizes
+// `grp` so that the group's K/V fit one XCD's 4 MB L2 (fill_attn): at N 16384 that is one head, i.e.
+// the per-head order, which measured 20 % faster there than level-major over all heads. With
+// nbh % 8 == 0 each XCD (bid & 7) keeps a contiguous range of heads, grouped inside the range;
+// otherwise the groups (of 8*grp heads) run over the whole grid. order 2 forces the whole-grid form.
+// Measurements: profiles/r1_fa_lpt_order.md.
+__device__ __forceinline__ void grouped_levels(int j, int nh, int nt, int grp, int& hd, int& lvl) {
+  const int g = grp < nh ? grp : nh;
+  const int gi = j / (g * nt), h0 = gi * g;
+  const int gs = nh - h0 < g ? nh - h0 : g;  // the last group may be short
+  const int r = j - gi * g * nt;
+  lvl = r / gs;
+  hd = h0 + r % gs;
+}
+
+__device__ __forceinline__ void tile_order(int bid, int nbh, int nt, int order, int grp, int& bh, int& lvl) {
   if (order == 1 && (nbh & 7) == 0) {
-    const int per = nbh >> 3, j = bid >> 3;
-    bh = (bid & 7) * per + j % per;
-    lvl = j / per;
+    const int per = nbh >> 3;
+    int hd;
+    grouped_levels(bid >> 3, per, nt, grp, hd, lvl);
+    bh = (bid & 7) * per + hd;
   } else if (order != 0) {
-    bh = bid % nbh;
-    lvl = bid / nbh;
+    grouped_levels(bid, nbh, nt, 8 * grp, bh, lvl);
   } else {
     const int rid = xcd_remap(bid, nbh * nt);
     bh = rid / nt;

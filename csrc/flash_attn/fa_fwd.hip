@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
 
   const int nqb = (p.Nq + BM - 1) / BM;
   int bh, qb;
-  tile_order(blockIdx.x, p.B * p.H, nqb, CAUSAL ? p.order : 0, bh, qb);
+  tile_order(blockIdx.x, p.B * p.H, nqb, CAUSAL ? p.order : 0, p.lpt_group, bh, qb);
   if (CAUSAL) qb = nqb - 1 - qb;
   const int b = bh / p.H, h = bh % p.H;
   const int q0 = qb * BM;

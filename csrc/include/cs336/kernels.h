@@ -115,6 +115,7 @@ struct AttnParams {
   // block dispatch order under the causal mask: 0 = per-(batch, head) interleaved, 1 = heaviest tile
   // level first within each XCD's heads (longest-processing-time order, see tile_order in fa_common.h)
   int order = 1;
+  int lpt_group = 1 << 20;  // heads per level-major group (sized by the host to the L2, fill_attn)
 };
 
 struct AttnBwdParams {

@@ -14,6 +14,8 @@ sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
 from cs336_systems.ops.flash_attention import FlashAttentionHIP  # noqa: E402
 
 SHAPES = [(3, 25, 4096, 64), (5, 25, 512, 64), (24, 25, 512, 64), (4, 12, 2048, 64), (2, 20, 4096, 128), (4, 16, 4096, 128)]
+if len(sys.argv) > 1:  # shapes as B,H,N,D ...
+    SHAPES = [tuple(int(x) for x in a.split(",")) for a in sys.argv[1:]]
 res = {}
 for B, H, N, D in SHAPES:
     torch.manual_seed(0)
