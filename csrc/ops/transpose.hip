@@ -1,18 +1,57 @@
 // 2-byte matrix transpose (bf16/f16) for MI355X: out[c][r] = in[r][c].
 //
 // Used to give the input-gradient GEMM a K-major copy of each projection weight (Wᵀ), the layout
-// hipBLASLt runs 1.15-1.4x faster (models/fused.py). 64×64 tiles through LDS: every global access
-// is a 16-byte chunk of a row (coalesced both ways); the LDS image is padded by one 16-B chunk per
-// row so the column gather spreads over the banks. Memory-bound: 2 B read + 2 B written per element.
+// hipBLASLt runs 1.15-1.4x faster, and the W1|W3 weight-gradient GEMM a token-contiguous Xᵀ
+// (models/fused.py). Memory-bound: 2 B read + 2 B written per element.
+//
+// Register transpose, no LDS: each thread loads an 8×8 block as eight 16-byte row chunks, transposes
+// it in VGPRs (16-bit lane packing, v_perm/v_and_or) and stores eight 16-byte column chunks. Lanes are
+// laid out chunk-fastest (ch = tid & 7, row group rr = tid >> 3), so within one wave every load
+// instruction reads eight 128-byte row runs and every store writes eight 128-byte output-row runs.
+// A workgroup covers 256 rows × 64 columns (32 KB), 4x the bytes in flight of the previous 64×64
+// LDS tile, and drops its eight 2-byte LDS gathers per stored chunk.
+#include <cstdlib>
+#include <string>
+
 #include "cs336/kernels.h"
 
 namespace cs336 {
 namespace {
 
+constexpr int kRows = 256;  // rows per workgroup (32 row groups of 8)
+constexpr int kCols = 64;   // columns per workgroup (8 chunks of 8)
+
+__device__ __forceinline__ uint32_t lo_pair(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
+__device__ __forceinline__ uint32_t hi_pair(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
+
+__global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* __restrict__ in, int64_t ld_in,
+                                                          uint16_t* __restrict__ out, int64_t ld_out, int R, int C) {
+  const int tid = threadIdx.x, ch = tid & 7, rr = tid >> 3;
+  const int r = blockIdx.y * kRows + 8 * rr;  // first of this thread's 8 input rows
+  const int c = blockIdx.x * kCols + 8 * ch;  // first of its 8 input columns
+  if (r >= R || c >= C) return;               // R, C are multiples of 8 (host check)
+  uint32_t v[8][4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint4 x = *reinterpret_cast<const uint4*>(in + (int64_t)(r + j) * ld_in + c);
+    v[j][0] = x.x; v[j][1] = x.y; v[j][2] = x.z; v[j][3] = x.w;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {  // output row c + k = input column c + k; element k sits in dword k/2
+    const int d = k >> 1;
+    uint32_t w[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      w[p] = (k & 1) ? hi_pair(v[2 * p][d], v[2 * p + 1][d]) : lo_pair(v[2 * p][d], v[2 * p + 1][d]);
+    *reinterpret_cast<uint4*>(out + (int64_t)(c + k) * ld_out + r) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// previous 64×64 LDS-tile version, kept for A/B (CS336_TRANSPOSE=lds)
 constexpr int kT = 64;        // tile edge
 constexpr int kLd = kT + 8;   // padded LDS row (elements): 144 B, keeps 16-B row alignment
 
-__global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* __restrict__ in, int64_t ld_in,
+__global__ __launch_bounds__(256) void transpose16_lds_kernel(const uint16_t* __restrict__ in, int64_t ld_in,
                                                           uint16_t* __restrict__ out, int64_t ld_out, int R, int C) {
   __shared__ __attribute__((aligned(16))) uint16_t t[kT * kLd];
   const int r0 = blockIdx.y * kT, c0 = blockIdx.x * kT, tid = threadIdx.x;
@@ -39,7 +78,16 @@ __global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* __rest
 }  // namespace
 
 void transpose16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int R, int C, hipStream_t s) {
-  const dim3 grid((unsigned)((C + kT - 1) / kT), (unsigned)((R + kT - 1) / kT)), block(256);
+  static const bool lds = [] {
+    const char* e = std::getenv("CS336_TRANSPOSE");
+    return e && std::string(e) == "lds";
+  }();
+  if (lds) {
+    const dim3 g((unsigned)((C + kT - 1) / kT), (unsigned)((R + kT - 1) / kT));
+    hipLaunchKernelGGL(transpose16_lds_kernel, g, dim3(256), 0, s, (const uint16_t*)in, ld_in, (uint16_t*)out, ld_out, R, C);
+    return;
+  }
+  const dim3 grid((unsigned)((C + kCols - 1) / kCols), (unsigned)((R + kRows - 1) / kRows)), block(256);
   hipLaunchKernelGGL(transpose16_kernel, grid, block, 0, s, (const uint16_t*)in, ld_in, (uint16_t*)out, ld_out, R, C);
 }
 
