@@ -1,0 +1,42 @@
+"""bench.py driver contract on CPU: launched the way the driver launches it (torch.distributed.run,
+one process per rank, 127.0.0.1 rendezvous), rank 0 prints exactly one JSON line whose fields match
+the world size. Uses gloo and the tiny model; the GPU run of the same code path is the driver's."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from cs336_systems.parallel.comm import find_free_port
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(nproc: int, *extra: str) -> list[dict]:
+    cmd = [
+        sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+        "--master-addr", "127.0.0.1", f"--master-port={find_free_port()}",
+        "bench.py", "--gpus", str(nproc), "--steps", "2", "--warmup", "1",
+        "--model", "tiny", "--ctx", "32", "--batch", "2", "--dtype", "fp32", *extra,
+    ]
+    env = dict(os.environ, CS336_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
+
+
+@pytest.mark.parametrize("nproc,extra", [(2, ()), (4, ()), (2, ("--sharded",))])
+def test_bench_multirank_json(nproc, extra):
+    lines = _run(nproc, *extra)
+    assert len(lines) == 1, lines
+    d = lines[0]
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in d
+    assert d["n_gpus"] == nproc and d["steps"] == 2 and d["warmup"] == 1
+    assert d["config"]["global_batch"] == 2 * nproc
+    assert d["config"]["parallelism"].startswith(f"dp{nproc}")
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["value"] == pytest.approx(2 * nproc * 32 / (d["ms_per_step"] / 1e3), rel=0.02)
