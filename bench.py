@@ -274,11 +274,14 @@ def main(argv=None):
         "peak_mem_gib": round(peak_gib, 2),
         "final_loss": round(last_loss, 4),
     }
+    if device.type != "cuda":  # CPU rehearsal: eager PyTorch reference ops, no HIP kernels ran
+        out["config"]["optimizer"] = out["config"]["optimizer"].replace("fused HIP AdamW", "PyTorch-reference AdamW")
+        out["config"]["attention"] = "PyTorch-reference attention (causal)"
     from cs336_systems.ops.gemm import _mode as gemm_mode
 
     gsel = {"blas": "hipblaslt default", "lt": "autotuned hipblaslt (cs336 lt_gemm)",
             "best": "per-problem faster of hipblaslt default / autotuned lt_gemm", "hip": "cs336 MFMA GEMM"}[gemm_mode()]
-    out["config"]["gemm_selection"] = f"tunableop:{tmode}" if tmode else gsel
+    out["config"]["gemm_selection"] = f"tunableop:{tmode}" if tmode else gsel if device.type == "cuda" else "torch cpu"
     if tmode == "tune" and rank == 0:
         import torch.cuda.tunable as tunable
 

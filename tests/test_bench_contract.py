@@ -39,4 +39,5 @@ def test_bench_multirank_json(nproc, extra):
     assert d["config"]["global_batch"] == 2 * nproc
     assert d["config"]["parallelism"].startswith(f"dp{nproc}")
     assert d["value"] > 0 and d["ms_per_step"] > 0
+    assert "HIP" not in d["config"]["attention"]  # CPU run must not claim the HIP kernels
     assert d["value"] == pytest.approx(2 * nproc * 32 / (d["ms_per_step"] / 1e3), rel=0.02)
