@@ -108,6 +108,48 @@ def setup_tunableop(mode: str, rank: int) -> str | None:
     return mode
 
 
+def dist_diagnostics(ddp_model, comm_wait_ms, device, world) -> dict:
+    """What a multi-GPU run needs to be diagnosable from its own JSON line: exposed communication
+    per step (max over ranks), the bucket layout, the process group as the ranks see it, the
+    RCCL version and environment, and a standalone all-reduce of the largest bucket (bus bandwidth
+    without compute beside it)."""
+    d: dict = {"pg_world_size": dist.get_world_size(), "backend": dist.get_backend()}
+    if comm_wait_ms is not None:
+        on_dev = dist.get_backend() == "nccl"
+        t = torch.tensor([comm_wait_ms], dtype=torch.float64, device=device if on_dev else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        d["comm_wait_ms"] = round(float(t.item()), 3)
+    buckets = ddp_model.bucket_summary() if hasattr(ddp_model, "bucket_summary") else []
+    if buckets:
+        mbs = [b["mb"] for b in buckets]
+        d["n_buckets"] = len(mbs)
+        d["bucket_mb"] = {"min": round(min(mbs), 2), "max": round(max(mbs), 2), "total": round(sum(mbs), 1)}
+        d["bucket_sizes_mb"] = [round(m, 1) for m in mbs]
+    try:
+        v = torch.cuda.nccl.version()
+        d["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception as e:  # noqa: BLE001 - diagnostic only
+        d["rccl_version"] = f"unavailable ({type(e).__name__})"
+    d["env"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith(("NCCL_", "RCCL_", "HSA_", "TORCH_NCCL_"))}
+    if buckets and world > 1 and device.type == "cuda" and dist.get_backend() == "nccl":
+        n = int(max(mbs) * 2**20 // 4)
+        buf = torch.ones(n, dtype=torch.float32, device=device)
+        for _ in range(2):
+            dist.all_reduce(buf)
+        torch.cuda.synchronize(device)
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dist.all_reduce(buf)
+        torch.cuda.synchronize(device)
+        dt = (time.perf_counter() - t0) / reps
+        algbw = n * 4 / dt / 1e9
+        d["allreduce_probe"] = {"mb": round(n * 4 / 2**20, 1), "ms": round(dt * 1e3, 3), "algbw_gbs": round(algbw, 1),
+                                "busbw_gbs": round(algbw * 2 * (world - 1) / world, 1)}
+        del buf
+    return d
+
+
 def main(argv=None):
     args = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -187,6 +229,11 @@ def main(argv=None):
 
         graphed = GraphedStep(loss_fn, model.parameters(), *batches[0])
 
+    # exposed communication: GPU time the compute stream spends waiting in
+    # finish_gradient_synchronization for collectives that backward did not hide (HIP events)
+    comm_events: list[tuple] = []
+    timing = {"on": False}
+
     def step(i):
         x, y = batches[i % len(batches)]
         if graphed is not None:  # captured forward + loss + backward, eager AdamW
@@ -199,7 +246,18 @@ def main(argv=None):
             loss = ops.cross_entropy(logits, y)
         loss.backward()
         if world > 1 or zero:
-            ddp_model.finish_gradient_synchronization()
+            if timing["on"] and device.type == "cuda":
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ddp_model.finish_gradient_synchronization()
+                e1.record()
+                comm_events.append((e0, e1))
+            elif timing["on"]:  # CPU/gloo: the wait blocks the host
+                t0 = time.perf_counter()
+                ddp_model.finish_gradient_synchronization()
+                comm_events.append(1e3 * (time.perf_counter() - t0))
+            else:
+                ddp_model.finish_gradient_synchronization()
         if args.clip > 0 and zero:
             ddp_model.clip_grad_norm_(args.clip)
         elif args.clip > 0:
@@ -223,13 +281,20 @@ def main(argv=None):
         torch.cuda.reset_peak_memory_stats(device)
     barrier()
     sync()
+    timing["on"] = True
     t_start = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
     sync()
     barrier()
     elapsed = time.perf_counter() - t_start
+    timing["on"] = False
     last_loss = loss.item()
+    comm_wait_ms = (
+        sum(e if isinstance(e, float) else e[0].elapsed_time(e[1]) for e in comm_events) / len(comm_events)
+        if comm_events
+        else None
+    )
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -243,7 +308,7 @@ def main(argv=None):
     mfu = value * flops_tok / (world * 2.5e15)
     cfg = get_model_config(args.model)
     out = {
-        "metric": METRIC,
+        "metric": METRIC if args.model == "xl" else METRIC.replace("GPT-2-XL", f"{args.model} (not the headline model)"),
         "value": round(value, 1),
         "unit": "tokens/s",
         "n_gpus": world,
@@ -282,6 +347,8 @@ def main(argv=None):
     gsel = {"blas": "hipblaslt default", "lt": "autotuned hipblaslt (cs336 lt_gemm)",
             "best": "per-problem faster of hipblaslt default / autotuned lt_gemm", "hip": "cs336 MFMA GEMM"}[gemm_mode()]
     out["config"]["gemm_selection"] = f"tunableop:{tmode}" if tmode else gsel if device.type == "cuda" else "torch cpu"
+    if world > 1 or zero:
+        out["dist"] = dist_diagnostics(ddp_model, comm_wait_ms, device, world)
     if tmode == "tune" and rank == 0:
         import torch.cuda.tunable as tunable
 

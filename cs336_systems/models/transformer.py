@@ -402,9 +402,23 @@ class BasicsTransformerLM(nn.Module):
         with annotate("lm_head"):
             return self.lm_head(self.ln_final(h))
 
+    def register_param_read_hook(self, fn) -> None:
+        """``fn(module)`` runs right before the fused-residual path reads ``module``'s parameters
+        WITHOUT calling its forward (the ln2 / next-ln1 / ln_final gains consumed by the fused
+        add+RMSNorm kernel), so forward pre-hooks would never see those reads. ZeRO-2 uses it to
+        wait for the all-gather of the bucket those weights live in (parallel/zero.py)."""
+        self.__dict__.setdefault("_param_read_hooks", []).append(fn)
+
+    def _reading(self, module: nn.Module) -> None:
+        for fn in self.__dict__.get("_param_read_hooks", ()):
+            fn(module)
+
     def _fused_residual_ok(self, h: torch.Tensor) -> bool:
         """The chained add+norm path needs the stock block/norm modules (no overridden forward,
-        e.g. the annotated or user-patched variants) and the HIP kernels."""
+        e.g. the annotated or user-patched variants) and the HIP kernels (or, for tests, an
+        explicit ``_force_fused_residual`` on CPU where ``ops.add_rmsnorm`` runs the eager ops)."""
+        if self.__dict__.get("_force_fused_residual") and len(self.layers):
+            return True
         if not (len(self.layers) and ops.use_hip(h)):
             return False
         norms = [self.ln_final] + [m for layer in self.layers for m in (layer.ln1, layer.ln2)]
@@ -423,10 +437,12 @@ class BasicsTransformerLM(nn.Module):
             with annotate(f"layer{i}"):
                 with annotate("block.attn"):
                     a = layer.attn(y, token_positions)
+                    self._reading(layer.ln2)
                     h, y = ops.add_rmsnorm(h, a, layer.ln2.weight, layer.ln2.eps)
                 with annotate("block.ffn"):
                     f = layer.ffn(y)
                     nxt = self.layers[i + 1].ln1 if i + 1 < n_layers else self.ln_final
+                    self._reading(nxt)
                     h, y = ops.add_rmsnorm(h, f, nxt.weight, nxt.eps)
         with annotate("lm_head"):
             return self.lm_head(y)

@@ -21,13 +21,23 @@ MI355X/RCCL design notes:
   host never blocks).
 * With the nccl(=RCCL) backend the mean is taken by ``ReduceOp.AVG`` inside the collective; Gloo
   (CPU tests) uses SUM followed by one in-place divide per flat bucket.
-* Bucket cap: xGMI is 7 point-to-point links per GPU (~153 GB/s each); RCCL only reaches its
-  multi-channel bus bandwidth with messages of tens of MB, while the last bucket's all-reduce is
-  exposed after backward. The default cap (``DEFAULT_BUCKET_MB``) balances those two; see
-  ``cs336_systems/bench/collectives.py`` for the size sweep that backs it.
+* Bucket cap (``DEFAULT_BUCKET_MB``) — derived, NOT yet measured on a multi-GPU RCCL node. The
+  handout's overhead model prices ``n_b`` buckets of a gradient of ``s`` bytes at
+  ``n_b·o + s/(w·n_b)``: a fixed launch/synchronisation cost ``o`` per collective plus the exposed
+  all-reduce of the last bucket at algorithm bandwidth ``w``. It is minimal at
+  ``bucket* = sqrt(s·w·o)``. For GPT-2 XL (s = 8.0 GB of fp32 gradients), an 8-rank RCCL ring over
+  xGMI (bus bandwidth ≈ 300 GB/s of the 7 × 153 GB/s links ⇒ w = busbw / (2·7/8) ≈ 170 GB/s) and
+  o ≈ 15-30 µs: bucket* ≈ 140-200 MB. 128 MB (64 buckets for XL) sits at the low edge, which keeps
+  the exposed tail of the last bucket (≈ 0.8 ms) small and costs ≈ 1-2 ms of per-collective
+  overhead spread over the backward. ``cs336_systems/bench/collectives.py`` measures ``w`` and
+  ``o`` on the node; only gloo/CPU numbers exist so far (``profiles/r1_allreduce_gloo_cpu.json``).
 * Unlike the reference, buckets hold only ``requires_grad`` parameters (no empty bucket 0, frozen
-  params never block a flush) and a bucket whose parameters received no gradient on this rank is
-  still reduced at ``finish_gradient_synchronization`` (zeros), so ranks never deadlock.
+  params never block a flush).
+* Collective order is identical on every rank: buckets are issued strictly in index order (a
+  bucket that completes early waits for its predecessors), and a bucket whose parameters received
+  no gradient on this rank is issued at ``finish_gradient_synchronization`` (zeros) in that same
+  order. RCCL pairs collectives by issue order, so an out-of-order launch on one rank (e.g. a
+  parameter unused on that rank only) would otherwise pair different buckets and hang.
 """
 
 from __future__ import annotations
@@ -239,6 +249,8 @@ class DDPBucketed(_DDPBase):
                 p._cs336_grad_out = self._views[p]
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in params]
         self._bucket_callbacks = []
+        self._next = 0  # index of the next bucket to issue
+        self._issued: list[int] = []
         self.zero_grad()
 
     def add_bucket_callback(self, fn) -> None:
@@ -269,6 +281,9 @@ class DDPBucketed(_DDPBase):
 
     # ---- hooks ------------------------------------------------------------------------------
     def _launch(self, b: _Bucket) -> None:
+        if b.idx == 0:
+            self._issued.clear()
+        self._issued.append(b.idx)
         with annotate(f"comm.bucket{b.idx}"):
             b.handle = self._all_reduce(b.flat, async_op=True)
         b.launched = True
@@ -279,23 +294,29 @@ class DDPBucketed(_DDPBase):
         b = self._param_bucket[p]
         self._adopt(p)
         b.pending -= 1
-        if b.pending == 0 and not b.launched:
-            self._launch(b)
+        # issue every leading complete bucket, strictly in index order (same order on every rank)
+        while self._next < len(self.buckets) and self.buckets[self._next].pending == 0:
+            self._launch(self.buckets[self._next])
+            self._next += 1
 
     def finish_gradient_synchronization(self) -> None:
-        # buckets with parameters that got no gradient on this rank are reduced now, in the same
-        # order on every rank (by bucket index)
-        for b in self.buckets:
-            if not b.launched:
-                for p in b.params:
-                    self._adopt(p)
-                self._launch(b)
+        # buckets with parameters that got no gradient on this rank are reduced now, continuing the
+        # index order
+        for b in self.buckets[self._next :]:
+            for p in b.params:
+                self._adopt(p)
+            self._launch(b)
+        self._next = 0
         for b in self.buckets:
             b.handle.wait()
             self._finish_mean(b.flat)
             b.handle = None
             b.launched = False
             b.pending = len(b.params)
+
+    def launch_order(self) -> list[int]:
+        """Bucket indices in the order their collectives were issued last step (tests)."""
+        return list(self._issued)
 
     def bucket_summary(self) -> list[dict]:
         return [

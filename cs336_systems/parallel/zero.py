@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ..models.fused import _SHADOW, mark_shadow_synced, sync_dw_stream
+from ..models.fused import _SHADOW, dw_stream_for, mark_shadow_synced, sync_dw_stream
 from ..ops.adamw import FusedAdamW, multi_tensor_l2norm
 from ..utils.profiling import annotate
 from .comm import broadcast_module_, supports_avg
@@ -154,11 +154,20 @@ class ZeroDDP(nn.Module):
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in params]
         # forward pre-hooks: wait for the all-gathers of the buckets a module's parameters live in
         self._fwd_hooks = []
+        self._module_buckets: dict[int, list[int]] = {}
         for m in module.modules():
             mine = {self._param_bucket[p].idx for p in m.parameters(recurse=m is not module) if p in self._param_bucket}
             if mine:
                 ids = sorted(mine, reverse=True)
+                self._module_buckets[id(m)] = ids
                 self._fwd_hooks.append(m.register_forward_pre_hook(lambda _m, _a, ids=ids: self._wait_buckets(ids)))
+        # parameters read without their module's forward (the fused add+RMSNorm path of
+        # BasicsTransformerLM reads ln2 / the next ln1 / ln_final gains directly): the model calls
+        # this right before such a read, so those buckets are waited for too
+        if hasattr(module, "register_param_read_hook"):
+            module.register_param_read_hook(lambda m: self._wait_buckets(self._module_buckets.get(id(m), ())))
+        self._next = 0  # next bucket to reduce-scatter (strict index order on every rank)
+        self._issued: list[int] = []
         self.zero_grad(set_to_none=False)
 
     def forward(self, *inputs, **kwargs):
@@ -190,29 +199,48 @@ class ZeroDDP(nn.Module):
         b = self._param_bucket[p]
         self._adopt(p)
         b.pending -= 1
-        if b.pending == 0 and not b.launched:
-            self._launch_rs(b)
+        # issue every leading complete bucket in index order: collectives pair by issue order, so
+        # every rank must issue the same sequence (a bucket finishing early waits its turn)
+        while self._next < len(self.buckets) and self.buckets[self._next].pending == 0:
+            self._launch_rs(self.buckets[self._next])
+            self._next += 1
 
     def _launch_rs(self, b: _ZBucket) -> None:
         b.launched = True
+        if b.idx == 0:
+            self._issued.clear()
+        self._issued.append(b.idx)
         if self._solo:
             return
         op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
-        sync_dw_stream()
         with annotate(f"comm.rs{b.idx}"):
             if b.staged:  # gloo cannot reduce-scatter HIP tensors: stage on the host
+                sync_dw_stream()
                 out = torch.empty(b.shard, dtype=torch.float32)
                 dist.reduce_scatter_tensor(out, b.gbuf.cpu(), op=op, group=self.process_group)
                 b.gshard.copy_(out)
-            else:
+                return
+            side = dw_stream_for(b.gbuf)
+            if side is None:
+                b.rs = dist.reduce_scatter_tensor(b.gshard, b.gbuf, op=op, group=self.process_group, async_op=True)
+                return
+            # weight gradients may still be in flight on the dW side stream: issue from that stream
+            # once it has caught up with the main stream (as DDPBucketed._all_reduce), so the main
+            # stream keeps running backward instead of waiting for every dW GEMM issued so far
+            side.wait_stream(torch.cuda.current_stream(b.gbuf.device))
+            with torch.cuda.stream(side):
                 b.rs = dist.reduce_scatter_tensor(b.gshard, b.gbuf, op=op, group=self.process_group, async_op=True)
 
+    def launch_order(self) -> list[int]:
+        """Bucket indices in the order their reduce-scatters were issued last step (tests)."""
+        return list(self._issued)
+
     def finish_gradient_synchronization(self) -> None:
-        for b in self.buckets:  # buckets with unused parameters: same order on every rank
-            if not b.launched:
-                for p in b.params:
-                    self._adopt(p)
-                self._launch_rs(b)
+        for b in self.buckets[self._next :]:  # buckets with unused parameters: continue the order
+            for p in b.params:
+                self._adopt(p)
+            self._launch_rs(b)
+        self._next = 0
         for b in self.buckets:
             if b.rs is not None:
                 b.rs.wait()

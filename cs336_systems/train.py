@@ -257,6 +257,9 @@ def train(cfg: TrainConfig) -> dict:
         if cfg.ckpt_dir and ((cfg.ckpt_every and done % cfg.ckpt_every == 0) or done == end):
             if zero:
                 ddp.wait_for_params()  # the parameter all-gathers of this step must land first
+            # never let a diverged state become `latest` (keep-N would then prune the good ones):
+            # this step's loss and the updated weights must be finite on every rank
+            _check_finite_before_save(loss, model, done, dev)
             if tp:  # the full weights (gathered) and one optimizer file per rank
                 save_checkpoint(cfg.ckpt_dir, done, model, opt, meta=dict(config=dataclasses.asdict(cfg)),
                                 model_state=gather_tp_state_dict(model), sharded=True)
@@ -265,6 +268,21 @@ def train(cfg: TrainConfig) -> dict:
     if log:
         log.close()
     return dict(rank=rank, world=world, start=start, history=hist, final_loss=loss_val)
+
+
+@torch.no_grad()
+def _check_finite_before_save(loss: torch.Tensor, model: torch.nn.Module, step: int, dev: torch.device) -> None:
+    """Raise on every rank if the loss or any (local) parameter is non-finite on any rank."""
+    from .ops.adamw import multi_tensor_l2norm
+
+    params = [p.detach() for p in model.parameters()]
+    sq = multi_tensor_l2norm(params).float().reshape(1) if params else torch.zeros(1, device=dev)
+    bad = (~torch.isfinite(loss.detach().float().reshape(1))) | (~torch.isfinite(sq))
+    flag = bad.to(torch.float32).to(dev)
+    if dist.is_initialized():
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    if flag.item() > 0:
+        raise FloatingPointError(f"non-finite loss or weights at step {step}; not checkpointing")
 
 
 def parse(argv=None) -> TrainConfig:

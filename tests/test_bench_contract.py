@@ -27,7 +27,7 @@ def _run(nproc: int, *extra: str) -> list[dict]:
     return [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
 
 
-@pytest.mark.parametrize("nproc,extra", [(2, ()), (4, ()), (2, ("--sharded",))])
+@pytest.mark.parametrize("nproc,extra", [(2, ()), (4, ()), (2, ("--sharded",)), (2, ("--ddp", "zero"))])
 def test_bench_multirank_json(nproc, extra):
     lines = _run(nproc, *extra)
     assert len(lines) == 1, lines
@@ -41,3 +41,10 @@ def test_bench_multirank_json(nproc, extra):
     assert d["value"] > 0 and d["ms_per_step"] > 0
     assert "HIP" not in d["config"]["attention"]  # CPU run must not claim the HIP kernels
     assert d["value"] == pytest.approx(2 * nproc * 32 / (d["ms_per_step"] / 1e3), rel=0.02)
+    # multi-rank diagnostics (the 8-GPU run must be diagnosable from its own line)
+    dd = d["dist"]
+    assert dd["pg_world_size"] == nproc and dd["backend"] == "gloo"
+    assert dd["comm_wait_ms"] >= 0
+    assert dd["n_buckets"] == len(dd["bucket_sizes_mb"]) >= 1
+    assert dd["bucket_mb"]["max"] <= 128.0 + 1e-6
+    assert "rccl_version" in dd and isinstance(dd["env"], dict)

@@ -1,0 +1,150 @@
+"""Collective-order safety of the bucketed data-parallel wrappers (gloo, CPU).
+
+1. A parameter that receives a gradient on rank 0 only: with buckets launched in completion order,
+   rank 1 would issue the buckets after it before the bucket holding it (which it can only issue
+   at ``finish_gradient_synchronization``) while rank 0 issues them in index order — collectives
+   pair by issue order, so the two ranks would reduce different buckets (wrong sums or a hang).
+   ``DDPBucketed`` and ``ZeroDDP`` issue strictly in bucket-index order; every rank's launch order
+   must be ``0..n-1`` and the result must equal single-process training.
+2. ZeRO-2 with the fused add+RMSNorm forward path (ln gains read without their module's forward):
+   the parameter all-gathers are made artificially slow (results land only at ``wait()``), so a
+   read that is not preceded by a wait sees the previous step's gains and the trained weights
+   diverge from single-process training.
+"""
+
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from cs336_systems.models import BasicsTransformerLM
+from cs336_systems.ops import FusedAdamW
+from cs336_systems.parallel import DDPBucketed
+from cs336_systems.parallel.zero import ZeroDDP
+
+from .common import spawn
+
+OPT = dict(lr=0.05, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1)
+
+
+class RankGatedModel(nn.Module):
+    """fc1 -> (+ side(x) on rank 0 only) -> fc2 -> fc3; with per-parameter buckets ``side`` sits
+    between buckets that complete during backward on every rank."""
+
+    def __init__(self):
+        super().__init__()
+        self.fc1 = nn.Linear(8, 16, bias=False)
+        self.side = nn.Linear(16, 16, bias=False)
+        self.fc2 = nn.Linear(16, 16, bias=False)
+        self.fc3 = nn.Linear(16, 4, bias=False)
+
+    def forward(self, x, use_side: bool):
+        h = torch.relu(self.fc1(x))
+        if use_side:
+            h = h + self.side(h)
+        return self.fc3(torch.relu(self.fc2(h)))
+
+
+def _init(rank, world):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _gated_worker(rank, world, kind):
+    _init(rank, world)
+    torch.manual_seed(0)
+    model = RankGatedModel()
+    ref = RankGatedModel()
+    ref.load_state_dict(model.state_dict())
+    if kind == "ddp":
+        wrapped = DDPBucketed(model, bucket_size_mb=0.0005)  # ≈ one parameter per bucket
+        opt = FusedAdamW(model.parameters(), **OPT)
+    else:
+        wrapped = ZeroDDP(model, bucket_size_mb=0.0005, **OPT)
+        opt = wrapped.optimizer
+    assert len(wrapped.buckets) >= 4
+    ref_opt = FusedAdamW(ref.parameters(), **OPT)
+    for it in range(3):
+        g = torch.Generator().manual_seed(it)
+        x = torch.randn(world * 4, 8, generator=g)
+        y = torch.randn(world * 4, 4, generator=g)
+        # reference: mean over ranks of each rank's loss (side branch on rank 0's slice only)
+        ref_opt.zero_grad(set_to_none=True)
+        loss = sum(F.mse_loss(ref(x[r * 4 : (r + 1) * 4], r == 0), y[r * 4 : (r + 1) * 4]) for r in range(world)) / world
+        loss.backward()
+        ref_opt.step()
+        opt.zero_grad(set_to_none=True)
+        xs, ys = x[rank * 4 : (rank + 1) * 4], y[rank * 4 : (rank + 1) * 4]
+        F.mse_loss(wrapped.module(xs, rank == 0), ys).backward()
+        wrapped.finish_gradient_synchronization()
+        assert wrapped.launch_order() == list(range(len(wrapped.buckets))), wrapped.launch_order()
+        opt.step()
+        sd = wrapped.state_dict() if kind == "zero" else model.state_dict()
+        for (n, a), b in zip(sd.items(), ref.state_dict().values()):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6, msg=lambda m, n=n, it=it: f"iter {it} {n}: {m}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("kind", ["ddp", "zero"])
+def test_param_unused_on_one_rank(kind):
+    spawn(_gated_worker, 2, kind)
+
+
+class _DeferredGather:
+    """Work handle whose result lands in the output only at ``wait()`` (a slow collective)."""
+
+    def __init__(self, out, res):
+        self.out, self.res = out, res
+
+    def wait(self):
+        self.out.copy_(self.res)
+        return True
+
+
+def _fused_residual_worker(rank, world):
+    _init(rank, world)
+    real_ag = dist.all_gather_into_tensor
+
+    def slow_ag(out, inp, group=None, async_op=False):
+        if not async_op:
+            return real_ag(out, inp, group=group)
+        res = torch.empty_like(out)
+        real_ag(res, inp, group=group)
+        return _DeferredGather(out, res)
+
+    dist.all_gather_into_tensor = slow_ag
+    cfg = dict(vocab_size=64, context_length=16, d_model=32, num_layers=2, num_heads=2, d_ff=64)
+    torch.manual_seed(0)
+    ref = BasicsTransformerLM(**cfg)
+    torch.manual_seed(0)
+    model = BasicsTransformerLM(**cfg)
+    model._force_fused_residual = True  # the GPU forward: ln gains read by ops.add_rmsnorm directly
+    zero = ZeroDDP(model, bucket_size_mb=0.004, **OPT)
+    assert len(zero.buckets) > 3
+    ref_opt = FusedAdamW(ref.parameters(), **OPT)
+    opt = zero.optimizer
+    for it in range(4):
+        g = torch.Generator().manual_seed(it)
+        x = torch.randint(0, 64, (2 * world, 16), generator=g)
+        ref_opt.zero_grad(set_to_none=True)
+        F.cross_entropy(ref(x).reshape(-1, 64), x.reshape(-1)).backward()
+        ref_opt.step()
+        opt.zero_grad(set_to_none=True)
+        xs = x[rank * 2 : (rank + 1) * 2]
+        F.cross_entropy(zero(xs).reshape(-1, 64), xs.reshape(-1)).backward()
+        zero.finish_gradient_synchronization()
+        opt.step()
+    for (name, a), b in zip(zero.state_dict().items(), ref.state_dict().values()):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4, msg=lambda m, n=name: f"{n}: {m}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_zero_fused_residual_waits_for_gathers():
+    spawn(_fused_residual_worker, 2)
