@@ -157,11 +157,19 @@ def compute_weight(params: list[nn.Parameter], dtype: torch.dtype) -> torch.Tens
 #
 # OFF by default (CS336_DW_STREAM=1 enables it). Measured on MI355X: it saves only ~2 ms of a
 # ~187 ms XL step, because the hipBLASLt GEMMs hold ~1 workgroup per CU and the HBM-bound kernels
-# next to them run 3-5x slower (profiles/r1_overlap_ab.json) — and with the 2.7b shapes at 12288
-# tokens (d_model 2560, d_ff 10240) two hipBLASLt GEMMs running concurrently on the two streams
-# never finished (the step hung in backward; serial streams, or AMD_SERIALIZE_KERNEL=3, complete in
-# 0.15 s). hipBLASLt's stream-K kernels assume they own the device, so concurrent GEMMs are not a
-# safe default.
+# next to them run 3-5x slower (profiles/r1_overlap_ab.json).
+#
+# Concurrent GEMMs and the round-1 hang: hipBLASLt's default picks for every projection GEMM are
+# stream-K Tensile kernels (SK3): a grid of <= 1 workgroup per CU in which the owner of a split tile
+# spins on a workspace flag written by the next-indexed workgroup (profiles/r2_streamk_hang.md). Two
+# of them on two streams need more slots than the chip has, each kernel's resident workgroups wait for
+# undispatched successors, and neither finishes -- the 2.7b step hung exactly so with the dW GEMMs on
+# this stream. hipBLASLt has no data-parallel alternative for these problems on gfx950 (2198 of
+# its 2199 solutions are stream-K, scripts/lt_dp_probe.py), so a weight gradient goes to the side
+# stream only if the cs336 MFMA GEMM (whole tiles per workgroup, no inter-workgroup waits) takes it
+# (gemm.dw_concurrent_ok); otherwise it runs on the main stream. A GEMM
+# beside a bounded occupant such as an RCCL kernel (which ends when its peers arrive) only waits
+# for it, it cannot deadlock (tests/test_concurrency_gpu.py).
 _SIDE_STREAMS: dict[int, torch.cuda.Stream] = {}
 _state = {"dirty": False, "callback": False}
 
@@ -330,17 +338,18 @@ class FusedLinearFn(torch.autograd.Function):
                 and dw_stream_enabled()
                 and all(p.grad is None for p in ctx.weights)
                 and all(dt == torch.float32 for dt in ctx.wdtype)
+                and gemm.dw_concurrent_ok(dy2, x2, ctx.xt)  # never a stream-K GEMM beside another GEMM
             )
             if ctx.xt:  # x2 holds Xᵀ (K_in, tokens)
-                dw_fn = lambda out=None: gemm.mm_tn_fp32_xt(dy2, x2, out=out)  # noqa: E731
+                dw_fn = lambda out=None, cs=False: gemm.mm_tn_fp32_xt(dy2, x2, out=out, concurrent_safe=cs)  # noqa: E731
             else:
-                dw_fn = lambda out=None: gemm.mm_tn_fp32(dy2, x2, out=out)  # noqa: E731
+                dw_fn = lambda out=None, cs=False: gemm.mm_tn_fp32(dy2, x2, out=out, concurrent_safe=cs)  # noqa: E731
             if side:
                 main = torch.cuda.current_stream(dy2.device)
                 s = _side_stream(dy2.device)
                 s.wait_stream(main)
                 with torch.cuda.stream(s):
-                    dw = dw_fn(target)
+                    dw = dw_fn(target, True)  # beside the main stream's GEMMs: no stream-K
                 dy2.record_stream(s)
                 x2.record_stream(s)
                 if target is None:

@@ -18,6 +18,14 @@ strides, output) problem is seen outside graph capture, ``torch.mm`` and the aut
 are each timed on it (HIP events on the current stream) and the winner is cached for the process.
 The sweep shows why neither alone is right: ``lt`` wins 1.2x on the QKV GEMMs and the lm_head weight
 gradient but loses 1.2x on the W1|W3 weight gradient from ``Xᵀ``.
+
+``concurrent_safe=True`` (weight-gradient GEMMs issued on the dW side stream, i.e. possibly beside
+another GEMM) runs the cs336 MFMA GEMM: every workgroup owns whole output tiles and never waits for
+another workgroup. hipBLASLt cannot be used there: on gfx950 2198 of the 2199 solutions of this
+problem type are stream-K kernels (``scripts/lt_dp_probe.py``), which keep at most one workgroup per
+CU and spin on flags set by later-dispatched workgroups of the same grid, so two of them sharing the
+chip can deadlock (``csrc/blas/lt_gemm.cpp``, ``profiles/r2_streamk_hang.md``).
+:func:`dw_concurrent_ok` says whether a weight gradient can go to the side stream at all.
 """
 
 from __future__ import annotations
@@ -111,9 +119,31 @@ def mm_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return torch.mm(dy, w)
 
 
-def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+NO_STREAM_K = 1  # lt_gemm flag: data-parallel hipBLASLt solutions only (none exist on gfx950 today)
+
+
+def dw_concurrent_ok(dy: torch.Tensor, x: torch.Tensor, xt_layout: bool) -> bool:
+    """Whether ``dW = dyᵀ·x`` can run beside another GEMM: the cs336 GEMM (no inter-workgroup
+    waits) must take the problem; the Xᵀ layout (K-major B) is not one of its orientations."""
+    return not xt_layout and ext_available() and _ok(dy, x, True, False)
+
+
+def _dw_concurrent(dy, x, out):
+    """Weight gradient with the cs336 MFMA GEMM (data-parallel tiles, safe beside other GEMMs)."""
+    if not _ok(dy, x, True, False):
+        raise RuntimeError(f"cs336 GEMM does not take the weight gradient {tuple(dy.shape)}ᵀ·{tuple(x.shape)}")
+    if out is None:
+        return ops().gemm(dy, x, True, False, torch.float32, 0, 0, 0)
+    ops().gemm_out(dy, x, True, False, out, False, 0, 0, 0)
+    return out
+
+
+def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None = None,
+                  concurrent_safe: bool = False) -> torch.Tensor:
     """``dy.T @ xt.T`` with an fp32 result: the weight gradient from a token-contiguous ``Xᵀ``
     (K_in, tokens). hipBLASLt only: its NT kernels are the fast ones for this layout."""
+    if concurrent_safe:
+        raise RuntimeError("no concurrency-safe GEMM for the Xᵀ weight-gradient layout (dw_concurrent_ok)")
     if lt_gemm_enabled() and _lt_ok(dy, xt) and (out is None or out.stride(1) == 1):
         if out is None:
             lt = lambda: ops().lt_gemm(dy, xt, True, True, torch.float32)  # noqa: E731
@@ -130,8 +160,11 @@ def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None =
     return torch.mm(dy.t(), xt.t(), out_dtype=torch.float32)
 
 
-def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
+               concurrent_safe: bool = False) -> torch.Tensor:
     """``dy.T @ x`` with an fp32 result (weight gradient), written into ``out`` when given."""
+    if concurrent_safe:
+        return _dw_concurrent(dy, x, out)
     if lt_gemm_enabled() and _lt_ok(dy, x) and (out is None or out.stride(1) == 1):
         if out is None:
             lt = lambda: ops().lt_gemm(dy, x, True, False, torch.float32)  # noqa: E731

@@ -632,6 +632,16 @@ void multi_tensor_scale_(std::vector<at::Tensor> tensors, const at::Tensor& scal
 
 }  // namespace
 
+// CU-occupying spin kernel (RCCL stand-in for concurrency tests), on the current stream
+void occupy(int64_t n_workgroups, int64_t lds_bytes, double ms, at::Tensor& counter) {
+  check_cuda(counter, "counter");
+  TORCH_CHECK(counter.scalar_type() == at::kInt && counter.numel() >= 1, "cs336: occupy counter must be int32");
+  TORCH_CHECK(n_workgroups > 0 && n_workgroups <= 65536 && lds_bytes >= 4 && lds_bytes <= 160 * 1024 && ms >= 0 &&
+                  ms <= 10000,
+              "cs336: occupy arguments out of range");
+  cs336::occupy((int)n_workgroups, (int)lds_bytes, ms, counter.data_ptr<int>(), stream());
+}
+
 TORCH_LIBRARY(cs336, m) {
   m.def(
       "fa_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None, "
@@ -665,6 +675,7 @@ TORCH_LIBRARY(cs336, m) {
       "adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, "
       "Tensor(d!)[] shadows, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("multi_tensor_l2norm(Tensor[] tensors) -> Tensor");
+  m.def("occupy(int n_workgroups, int lds_bytes, float ms, Tensor(a!) counter) -> ()");
   m.def("multi_tensor_scale_(Tensor(a!)[] tensors, Tensor scale) -> ()");
 }
 
@@ -690,5 +701,6 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("xent_bwd", &xent_bwd);
   m.impl("adamw_step", &adamw_step);
   m.impl("multi_tensor_l2norm", &multi_tensor_l2norm);
+  m.impl("occupy", &occupy);
   m.impl("multi_tensor_scale_", &multi_tensor_scale_);
 }

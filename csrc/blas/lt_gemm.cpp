@@ -17,15 +17,28 @@
 //   out = op(a) · op(b);  op(a): M x K (a stored K x M when a_t),  op(b): K x N (b stored N x K when b_t)
 //
 // Only beta = 0 (overwrite) -- the weight gradients are written straight into their DDP bucket slot.
+//
+// flags & kNoStreamK: only non-stream-K solutions. hipBLASLt's default picks for the projection
+// GEMMs are stream-K Tensile kernels ("SK3" in the kernel name): a grid of at most one workgroup
+// per CU (124 KB of LDS each), where a workgroup that owns a split tile spins on a workspace flag
+// that the NEXT-indexed workgroup sets when its partial sum is written (label_SK_Fixup in the
+// disassembly, profiles/r2_streamk_hang.md). That is only deadlock-free while the whole grid is
+// co-resident. Two such GEMMs on two streams need ~2x256 slots of a 256-slot chip: each kernel's
+// resident workgroups wait for its own undispatched successors and neither can finish -- the
+// round-1 hang of the 2.7b step with weight-gradient GEMMs on a side stream. GEMMs that may run
+// concurrently with another GEMM therefore use data-parallel (SK0) solutions.
 
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/HIPContextLight.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>
 #include <torch/library.h>
 
+#include <algorithm>
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -42,21 +55,25 @@ namespace {
     TORCH_CHECK(_s == HIPBLAS_STATUS_SUCCESS, "hipBLASLt error ", int(_s), " at " #expr);       \
   } while (0)
 
+constexpr int64_t kNoStreamK = 1;
+
 struct Key {
   int64_t m, n, k, lda, ldb, ldo;
   bool a_t, b_t;
   int out;  // hipDataType of the output
   int dev;
+  int64_t flags;
   bool operator==(const Key& o) const {
     return m == o.m && n == o.n && k == o.k && lda == o.lda && ldb == o.ldb && ldo == o.ldo && a_t == o.a_t &&
-           b_t == o.b_t && out == o.out && dev == o.dev;
+           b_t == o.b_t && out == o.out && dev == o.dev && flags == o.flags;
   }
 };
 
 struct KeyHash {
   size_t operator()(const Key& k) const {
     size_t h = 1469598103934665603ull;
-    for (int64_t v : {k.m, k.n, k.k, k.lda, k.ldb, k.ldo, int64_t(k.a_t), int64_t(k.b_t), int64_t(k.out), int64_t(k.dev)})
+    for (int64_t v : {k.m, k.n, k.k, k.lda, k.ldb, k.ldo, int64_t(k.a_t), int64_t(k.b_t), int64_t(k.out), int64_t(k.dev),
+                      k.flags})
       h = (h ^ size_t(v)) * 1099511628211ull;
     return h;
   }
@@ -71,7 +88,28 @@ struct Plan {
   bool tuned = false;
   float best_us = 0.f, first_us = 0.f;
   int n_cand = 0, best_idx = 0;
+  std::string kernel;  // Tensile kernel name of the chosen algorithm
 };
+
+// Stream-K mode from a Tensile kernel name: the value of its "SK<n>" token (0 = data-parallel).
+int stream_k_mode(const std::string& name) {
+  size_t pos = 0;
+  while ((pos = name.find("_SK", pos)) != std::string::npos) {
+    size_t i = pos + 3, j = i;
+    while (j < name.size() && std::isdigit(static_cast<unsigned char>(name[j]))) ++j;
+    if (j > i && (j == name.size() || name[j] == '_')) return std::atoi(name.substr(i, j - i).c_str());
+    pos = i;
+  }
+  return 0;
+}
+
+std::string kernel_name(hipblasLtHandle_t h, hipblasLtMatmulAlgo_t& algo) {
+  try {
+    return hipblaslt_ext::getKernelNameFromAlgo(h, algo);
+  } catch (...) {
+    return std::string();
+  }
+}
 
 std::mutex g_mu;
 std::unordered_map<Key, Plan, KeyHash> g_plans;
@@ -108,23 +146,86 @@ void run(hipblasLtHandle_t h, Plan& p, const hipblasLtMatmulAlgo_t* algo, const 
   LT_CHECK(launch(h, p, algo, a, b, out, ws, ws_bytes, s));
 }
 
+// Macro-tile area from a Tensile kernel name ("..._MT160x256x64_..." -> 160*256), 0 if absent.
+int64_t macro_tile_area(const std::string& name) {
+  const size_t pos = name.find("_MT");
+  if (pos == std::string::npos) return 0;
+  long a = 0, b = 0;
+  if (std::sscanf(name.c_str() + pos + 3, "%ldx%ld", &a, &b) != 2) return 0;
+  return int64_t(a) * int64_t(b);
+}
+
+// The heuristic's top candidates for the big projection GEMMs are all stream-K; enumerate every
+// solution of the problem type instead and keep the supported data-parallel ones, largest macro
+// tiles first (these GEMMs are large), at most CS336_LT_DP_CANDIDATES of them for timing.
+void all_data_parallel(hipblasLtHandle_t h, Plan& p, const Key& k, size_t ws_bytes,
+                       std::vector<hipblasLtMatmulHeuristicResult_t>& res, std::vector<std::string>& names) {
+  std::vector<hipblasLtMatmulHeuristicResult_t> cands;
+  const hipblasOperation_t ta = k.b_t ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = k.a_t ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  LT_CHECK(hipblaslt_ext::getAllAlgos(h, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, ta, tb, HIP_R_16BF, HIP_R_16BF,
+                                      hipDataType(k.out), hipDataType(k.out), HIPBLAS_COMPUTE_32F, cands));
+  const float alpha = 1.f, beta = 0.f;
+  std::vector<std::tuple<int64_t, size_t>> keep;  // (tile area, index)
+  std::vector<std::string> cn(cands.size());
+  for (size_t i = 0; i < cands.size(); ++i) {
+    cn[i] = kernel_name(h, cands[i].algo);
+    if (cn[i].empty() || stream_k_mode(cn[i]) != 0) continue;
+    size_t ws = 0;
+    if (hipblaslt_ext::matmulIsAlgoSupported(h, p.op, &alpha, p.la, p.lb, &beta, p.lo, p.lo, cands[i].algo, ws) !=
+            HIPBLAS_STATUS_SUCCESS ||
+        ws > ws_bytes)
+      continue;
+    cands[i].workspaceSize = ws;
+    cands[i].state = HIPBLAS_STATUS_SUCCESS;
+    keep.emplace_back(macro_tile_area(cn[i]), i);
+  }
+  std::stable_sort(keep.begin(), keep.end(), [](const auto& x, const auto& y) { return std::get<0>(x) > std::get<0>(y); });
+  if (env_int("CS336_LT_VERBOSE", 0)) {
+    int n_sk = 0, n_unnamed = 0;
+    for (const auto& nm : cn) n_unnamed += nm.empty(), n_sk += !nm.empty() && stream_k_mode(nm) != 0;
+    std::fprintf(stderr, "[lt] %ldx%ldx%ld all-algos: %zu total, %d stream-K, %d unnamed, %zu data-parallel supported\n",
+                 long(k.m), long(k.n), long(k.k), cands.size(), n_sk, n_unnamed, keep.size());
+    for (size_t i = 0; i < cands.size() && i < 6; ++i) std::fprintf(stderr, "[lt]   e.g. %s\n", cn[i].c_str());
+  }
+  const size_t cap = size_t(std::max(1, env_int("CS336_LT_DP_CANDIDATES", 96)));
+  for (size_t j = 0; j < keep.size() && j < cap; ++j) {
+    res.push_back(cands[std::get<1>(keep[j])]);
+    names.push_back(cn[std::get<1>(keep[j])]);
+  }
+}
+
 void tune(hipblasLtHandle_t h, Plan& p, const Key& k, const void* a, const void* b, void* out, void* ws, size_t ws_bytes,
           hipStream_t s, bool capturing) {
   hipblasLtMatmulPreference_t pref;
   LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
   uint64_t wsb = ws_bytes;
   LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)));
-  const int want = capturing ? 1 : std::max(1, env_int("CS336_LT_CANDIDATES", 48));
-  std::vector<hipblasLtMatmulHeuristicResult_t> res(want);
-  int got = 0;
-  LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.la, p.lb, p.lo, p.lo, pref, want, res.data(), &got));
+  const bool no_sk = (k.flags & kNoStreamK) != 0;
+  // (stream-K candidates are dropped below when no_sk: ask for more so data-parallel ones remain)
+  const int want = no_sk ? std::max(64, env_int("CS336_LT_CANDIDATES", 48))
+                         : (capturing ? 1 : std::max(1, env_int("CS336_LT_CANDIDATES", 48)));
+  std::vector<hipblasLtMatmulHeuristicResult_t> all(want);
+  int got_all = 0;
+  LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.la, p.lb, p.lo, p.lo, pref, want, all.data(), &got_all));
   hipblasLtMatmulPreferenceDestroy(pref);
-  TORCH_CHECK(got > 0, "hipBLASLt: no algorithm for ", k.m, "x", k.n, "x", k.k);
+  std::vector<hipblasLtMatmulHeuristicResult_t> res;
+  std::vector<std::string> names;
+  for (int i = 0; i < got_all; ++i) {
+    std::string nm = kernel_name(h, all[i].algo);
+    if (no_sk && (nm.empty() || stream_k_mode(nm) != 0)) continue;
+    res.push_back(all[i]);
+    names.push_back(std::move(nm));
+  }
+  if (no_sk && res.empty()) all_data_parallel(h, p, k, ws_bytes, res, names);
+  const int got = int(res.size());
+  TORCH_CHECK(got > 0, "hipBLASLt: no ", no_sk ? "data-parallel (non-stream-K) " : "", "algorithm for ", k.m, "x",
+              k.n, "x", k.k, " among ", got_all, " candidates");
   p.n_cand = got;
   if (capturing || got == 1) {
     // Cannot time inside a capture: use the heuristic's first choice, retune on the next eager call.
     p.algo = res[0].algo;
     p.ws = res[0].workspaceSize;
+    p.kernel = names[0];
     p.tuned = !capturing;
     return;
   }
@@ -157,6 +258,7 @@ void tune(hipblasLtHandle_t h, Plan& p, const Key& k, const void* a, const void*
   (void)hipEventDestroy(e1);
   p.algo = res[best_i].algo;
   p.ws = res[best_i].workspaceSize;
+  p.kernel = names[best_i];
   p.best_us = best;
   p.best_idx = best_i;
   p.tuned = true;
@@ -165,7 +267,32 @@ void tune(hipblasLtHandle_t h, Plan& p, const Key& k, const void* a, const void*
                  long(k.k), best_i, best, p.first_us);
 }
 
+Plan* plan_for(const at::Tensor& a, const at::Tensor& b, bool a_t, bool b_t, const at::Tensor& out, int64_t flags,
+               bool* empty);
+
+void lt_gemm_out_ex(const at::Tensor& a, const at::Tensor& b, bool a_t, bool b_t, at::Tensor& out, int64_t flags) {
+  bool empty = false;
+  Plan* p = plan_for(a, b, a_t, b_t, out, flags, &empty);
+  if (empty) return;
+  hipblasLtHandle_t h = at::cuda::getCurrentCUDABlasLtHandle();
+  run(h, *p, &p->algo, a.data_ptr(), b.data_ptr(), out.data_ptr(), at::cuda::getCUDABlasLtWorkspace(),
+      at::cuda::getCUDABlasLtWorkspaceSize(), at::hip::getCurrentHIPStream());
+}
+
 void lt_gemm_out(const at::Tensor& a, const at::Tensor& b, bool a_t, bool b_t, at::Tensor& out) {
+  lt_gemm_out_ex(a, b, a_t, b_t, out, 0);
+}
+
+// Kernel name of the plan the op would run for this problem (tunes it first if needed).
+std::string lt_gemm_kernel(const at::Tensor& a, const at::Tensor& b, bool a_t, bool b_t, at::Tensor& out,
+                           int64_t flags) {
+  bool empty = false;
+  Plan* p = plan_for(a, b, a_t, b_t, out, flags, &empty);
+  return empty ? std::string() : p->kernel;
+}
+
+Plan* plan_for(const at::Tensor& a, const at::Tensor& b, bool a_t, bool b_t, const at::Tensor& out, int64_t flags,
+               bool* empty) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "lt_gemm_out: CUDA tensors expected");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "lt_gemm_out: bf16 operands");
   TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "lt_gemm_out: fp32/bf16 out");
@@ -174,13 +301,17 @@ void lt_gemm_out(const at::Tensor& a, const at::Tensor& b, bool a_t, bool b_t, a
   const int64_t M = a_t ? a.size(1) : a.size(0), K = a_t ? a.size(0) : a.size(1);
   const int64_t N = b_t ? b.size(0) : b.size(1), Kb = b_t ? b.size(1) : b.size(0);
   TORCH_CHECK(K == Kb && out.size(0) == M && out.size(1) == N, "lt_gemm_out: shape mismatch");
-  if (M == 0 || N == 0) return;
+  if (M == 0 || N == 0) {
+    *empty = true;
+    return nullptr;
+  }
   if (K == 0) {
-    out.zero_();
-    return;
+    const_cast<at::Tensor&>(out).zero_();
+    *empty = true;
+    return nullptr;
   }
   const Key key{M, N, K, a.stride(0), b.stride(0), out.stride(0), a_t, b_t,
-                int(out.scalar_type() == at::kFloat ? HIP_R_32F : HIP_R_16BF), a.get_device()};
+                int(out.scalar_type() == at::kFloat ? HIP_R_32F : HIP_R_16BF), a.get_device(), flags};
   hipStream_t s = at::hip::getCurrentHIPStream();
   hipblasLtHandle_t h = at::cuda::getCurrentCUDABlasLtHandle();
   void* ws = at::cuda::getCUDABlasLtWorkspace();
@@ -196,14 +327,19 @@ void lt_gemm_out(const at::Tensor& a, const at::Tensor& b, bool a_t, bool b_t, a
     p = &it->second;
     if (!p->tuned) tune(h, *p, key, a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, ws_bytes, s, capturing);
   }
-  run(h, *p, &p->algo, a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, ws_bytes, s);
+  return p;
+}
+
+at::Tensor lt_gemm_ex(const at::Tensor& a, const at::Tensor& b, bool a_t, bool b_t, at::ScalarType out_dtype,
+                      int64_t flags) {
+  const int64_t M = a_t ? a.size(1) : a.size(0), N = b_t ? b.size(0) : b.size(1);
+  at::Tensor out = at::empty({M, N}, a.options().dtype(out_dtype));
+  lt_gemm_out_ex(a, b, a_t, b_t, out, flags);
+  return out;
 }
 
 at::Tensor lt_gemm(const at::Tensor& a, const at::Tensor& b, bool a_t, bool b_t, at::ScalarType out_dtype) {
-  const int64_t M = a_t ? a.size(1) : a.size(0), N = b_t ? b.size(0) : b.size(1);
-  at::Tensor out = at::empty({M, N}, a.options().dtype(out_dtype));
-  lt_gemm_out(a, b, a_t, b_t, out);
-  return out;
+  return lt_gemm_ex(a, b, a_t, b_t, out_dtype, 0);
 }
 
 // [m, n, k, a_t, b_t, out_dtype_code, n_candidates, best_index, best_ns, heuristic_first_ns] per tuned problem.
@@ -227,9 +363,17 @@ TORCH_LIBRARY_FRAGMENT(cs336, m) {
   m.def("lt_gemm(Tensor a, Tensor b, bool a_t, bool b_t, ScalarType out_dtype) -> Tensor");
   m.def("lt_gemm_out(Tensor a, Tensor b, bool a_t, bool b_t, Tensor(a!) out) -> ()");
   m.def("lt_gemm_table() -> int[]", &lt_gemm_table);
+  // flags: 1 = data-parallel (non-stream-K) solutions only (safe beside another GEMM on another stream)
+  m.def("lt_gemm_ex(Tensor a, Tensor b, bool a_t, bool b_t, ScalarType out_dtype, int flags) -> Tensor");
+  m.def("lt_gemm_out_ex(Tensor a, Tensor b, bool a_t, bool b_t, Tensor(a!) out, int flags) -> ()");
+  m.def("lt_gemm_kernel(Tensor a, Tensor b, bool a_t, bool b_t, Tensor out, int flags) -> str");
+  m.def("tensile_stream_k_mode(str kernel_name) -> int", [](const std::string& n) { return int64_t(stream_k_mode(n)); });
 }
 
 TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("lt_gemm", &lt_gemm);
   m.impl("lt_gemm_out", &lt_gemm_out);
+  m.impl("lt_gemm_ex", &lt_gemm_ex);
+  m.impl("lt_gemm_out_ex", &lt_gemm_out_ex);
+  m.impl("lt_gemm_kernel", &lt_gemm_kernel);
 }

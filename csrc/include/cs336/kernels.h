@@ -28,6 +28,10 @@ void rmsnorm_bwd_add(const void* dy, DType dyt, const void* x, DType xt, const f
 // 16-B aligned rows
 void transpose16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int R, int C, hipStream_t s);
 
+// ---- diagnostics (csrc/ops/occupy.hip): n_workgroups x 256 threads, each holding lds_bytes of LDS,
+// spin for `ms` of wall-clock time, then atomically increment *done
+void occupy(int n_workgroups, int lds_bytes, double ms, int* done, hipStream_t s);
+
 // ---- bf16 MFMA GEMM (csrc/gemm/gemm.hip) ----
 // C[M][N] = Σ_k A(m,k) B(k,n); A(m,k) = a[m·lda+k] (K-major) or a[k·lda+m]; B(k,n) = b[n·ldb+k]
 // (K-major) or b[k·ldb+n]. out_mode 0: bf16 C, 1: fp32 C, 2: fp32 C += . splits > 1: fp32 slabs
