@@ -203,7 +203,8 @@ def main(argv=None):
         opt = ddp_model.optimizer
         overlap = False
     elif args.sharded and world > 1:
-        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw)
+        # in-place async parameter all-gather, waited for by the next forward (stream dependency)
+        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw).attach(ddp_model)
         overlap = False
     else:
         opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)

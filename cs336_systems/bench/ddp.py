@@ -65,7 +65,7 @@ def train_ddp(rank: int, world: int, args) -> dict | None:
     # bf16 weight shadows (models/fused.py) whenever the step runs under bf16 autocast on GPU
     shadows = (not args.cpu) and args.dtype == "bf16" and dev.type == "cuda"
     if args.sharded:
-        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw)
+        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw).attach(ddp)
     else:
         opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)
         if args.overlap_opt and args.clip == 0:

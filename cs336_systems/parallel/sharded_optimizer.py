@@ -11,11 +11,21 @@ Semantics kept from the reference:
 
 MI355X-first changes:
 
-* after the local step, updated parameters are shipped with **one all-gather per dtype**
-  (``all_gather_into_tensor`` of each rank's packed shard, padded to the largest shard) plus a
-  single multi-tensor copy to unpack, instead of one broadcast per parameter (291-435 RCCL
-  launches per step for the 2.7b/XL models in the reference). Packing/unpacking are pure copies,
-  so values stay exact;
+* **owner-contiguous flat storage.** At construction every parameter is re-homed (``p.data =`` a
+  view) into one flat buffer per (device, dtype), laid out rank-major: rank 0's parameters, then
+  rank 1's, ..., each rank's region padded to the largest one. Parameters sharing one storage (the
+  fused QKV / W1|W3 row blocks of ``models/fused.py``) are one ownership unit and stay adjacent, so
+  the grouped GEMMs keep their single-tensor views;
+* **one in-place all-gather per dtype, asynchronous.** After the local step the flat buffer is
+  all-gathered in place (``all_gather_into_tensor(flat, flat[own region])``): no pack (``torch.cat``)
+  or unpack (``_foreach_copy_``) pass, one RCCL launch instead of one broadcast per parameter
+  (291-435 per step for the 2.7b/XL models in the reference). On RCCL the gather is not waited for
+  by the host: :meth:`attach` registers a forward pre-hook on the model that makes the compute
+  stream wait for it right before the next forward (so zero-grad memsets and host work overlap
+  it); without an attached module the wait is issued at the end of ``step``. Gloo waits at once;
+* values stay exact (pure copies), so results are bit-identical to the unsharded optimizer;
+* bf16 compute shadows (``bf16_shadows=True``) mirror the flat layout; the owned region's shadows are
+  written by the update kernel, the gathered regions are re-cast in one multi-tensor launch;
 * a rank that owns no parameters still participates (the reference crashed on ``None``);
 * hyper-parameter edits on ``self.param_groups`` (LR schedules) are forwarded to the local
   optimizer every step.
@@ -41,30 +51,83 @@ class ShardedOptimizer(torch.optim.Optimizer):
         self.param_to_rank: dict[int, int] = {}
         self.rank_sizes = [0] * self.world_size
         self._local_group_of: dict[int, int] = {}  # global group idx -> local group idx
-        self._sync_plan = None
-        params = list(params)
+        self._flats: list[dict] = []
+        self._pending: list = []  # in-flight all-gather works
+        self._attached = False
         self._shadows = bool(kwargs.get("bf16_shadows", False))
+        params = list(params)
+        if params and isinstance(params[0], dict):
+            groups = [{**g, "params": list(g["params"])} for g in params]
+        else:
+            groups = [{"params": params}]
+        self._assign_and_rehome([p for g in groups for p in g["params"]])
         if self._shadows:
-            # bf16 compute-weight shadows for EVERY replica parameter (grouped weights share one
-            # shadow storage): the local optimizer rewrites its owned shadows in the update kernel,
-            # the all-gathered ones are re-cast in one multi-tensor launch after the sync
+            # bf16 compute-weight shadows for EVERY replica parameter; one shadow storage per flat
+            # buffer, so the shadow layout is the flat layout
             from ..models.fused import attach_bf16_shadows
 
-            flat = [p for g in params for p in (g["params"] if isinstance(g, dict) else [g])]
-            attach_bf16_shadows(flat)
-        super().__init__(params, defaults=dict(kwargs))
+            attach_bf16_shadows([p for g in groups for p in g["params"]])
+        super().__init__(groups, defaults=dict(kwargs))
 
     # ------------------------------------------------------------------------------------------
+    def _assign_and_rehome(self, params: list[torch.Tensor]) -> None:
+        """Owner per storage unit (greedy: fewest owned bytes so far, in parameter order), then
+        re-home every parameter into a rank-major flat buffer per (device, dtype)."""
+        seen: set[int] = set()
+        uniq = []
+        for p in params:
+            if id(p) not in seen:
+                seen.add(id(p))
+                uniq.append(p)
+        units: dict[int, list[torch.Tensor]] = {}
+        order: list[int] = []
+        for p in uniq:
+            key = p.untyped_storage().data_ptr() if p.numel() else id(p)
+            if key not in units:
+                units[key] = []
+                order.append(key)
+            units[key].append(p)
+        by_kind: dict[tuple, list[list[list[torch.Tensor]]]] = {}
+        for key in order:
+            unit = sorted(units[key], key=lambda t: t.storage_offset())
+            nbytes = sum(p.numel() * p.element_size() for p in unit)
+            owner = min(range(self.world_size), key=lambda r: (self.rank_sizes[r], r))
+            self.rank_sizes[owner] += nbytes
+            for p in unit:
+                self.param_to_rank[id(p)] = owner
+            kind = (unit[0].device, unit[0].dtype)
+            by_kind.setdefault(kind, [[] for _ in range(self.world_size)])[owner].append(unit)
+        with torch.no_grad():
+            for (dev, dtype), per_rank in by_kind.items():
+                sizes = [sum(p.numel() for u in us for p in u) for us in per_rank]
+                smax = max(sizes)
+                if smax == 0:
+                    continue
+                flat = torch.zeros(smax * self.world_size, device=dev, dtype=dtype)
+                for r, us in enumerate(per_rank):
+                    off = r * smax
+                    for u in us:
+                        for p in u:
+                            n = p.numel()
+                            flat[off : off + n].copy_(p.detach().reshape(-1))
+                            p.data = flat[off : off + n].view_as(p)
+                            off += n
+                self._flats.append(dict(flat=flat, smax=smax, sizes=sizes,
+                                        params=[p for us in per_rank for u in us for p in u],
+                                        mine=[p for u in per_rank[self.rank] for p in u]))
+
     def add_param_group(self, param_group: dict[str, Any]) -> None:
         super().add_param_group(param_group)
         g = self.param_groups[-1]
         gidx = len(self.param_groups) - 1
         local = []
         for p in g["params"]:
-            owner = min(range(self.world_size), key=lambda r: (self.rank_sizes[r], r))
-            self.param_to_rank[id(p)] = owner
-            self.rank_sizes[owner] += p.numel() * p.element_size()
-            if owner == self.rank:
+            if id(p) not in self.param_to_rank:  # a group added after construction: no re-homing
+                owner = min(range(self.world_size), key=lambda r: (self.rank_sizes[r], r))
+                self.param_to_rank[id(p)] = owner
+                self.rank_sizes[owner] += p.numel() * p.element_size()
+                self._late = getattr(self, "_late", []) + [p]
+            if self.param_to_rank[id(p)] == self.rank:
                 local.append(p)
         if local:
             cfg = {k: v for k, v in g.items() if k != "params"}
@@ -74,10 +137,15 @@ class ShardedOptimizer(torch.optim.Optimizer):
             else:
                 self.optimizer.add_param_group(lg)
             self._local_group_of[gidx] = len(self.optimizer.param_groups) - 1
-        self._sync_plan = None
 
     def owner_of(self, p: torch.Tensor) -> int:
         return self.param_to_rank[id(p)]
+
+    def attach(self, module: torch.nn.Module) -> "ShardedOptimizer":
+        """Defer the wait for the parameter all-gather to the start of ``module``'s next forward."""
+        module.register_forward_pre_hook(lambda _m, _a: self.wait_parameters())
+        self._attached = True
+        return self
 
     # ------------------------------------------------------------------------------------------
     def _forward_hparams(self) -> None:
@@ -91,6 +159,7 @@ class ShardedOptimizer(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure: Callable | None = None, **kwargs):
+        self.wait_parameters()  # a previous gather must land before the owned region changes
         self._forward_hparams()
         loss = None
         if self.optimizer is not None:
@@ -102,54 +171,46 @@ class ShardedOptimizer(torch.optim.Optimizer):
         return loss
 
     # ------------------------------------------------------------------------------------------
-    def _build_plan(self):
-        """Per (device, dtype): params of every rank in global order, shard sizes, buffers."""
-        plan = {}
-        for g in self.param_groups:
-            for p in g["params"]:
-                key = (p.device, p.dtype)
-                plan.setdefault(key, [[] for _ in range(self.world_size)])[self.param_to_rank[id(p)]].append(p)
-        out = []
-        for (dev, dtype), per_rank in plan.items():
-            sizes = [sum(p.numel() for p in ps) for ps in per_rank]
-            smax = max(sizes) if sizes else 0
-            if smax == 0:
-                continue
-            send = torch.empty(smax, device=dev, dtype=dtype)
-            recv = torch.empty(smax * self.world_size, device=dev, dtype=dtype)
-            out.append((per_rank, sizes, smax, send, recv))
-        self._sync_plan = out
-
     @torch.no_grad()
     def sync_parameters(self) -> None:
-        """All-gather every rank's updated shard and copy the values into the replicas."""
+        """All-gather every rank's updated region of each flat buffer in place (async on RCCL)."""
         if self.world_size == 1:
             return
-        if self._sync_plan is None:
-            self._build_plan()
-        for per_rank, sizes, smax, send, recv in self._sync_plan:
-            mine = per_rank[self.rank]
-            if mine:
-                torch.cat([p.detach().reshape(-1) for p in mine], out=send[: sizes[self.rank]])
-            dist.all_gather_into_tensor(recv, send, group=self.process_group)
-            dst, src, received = [], [], []
-            for r in range(self.world_size):
-                if r == self.rank or not per_rank[r]:
-                    continue
-                off = r * smax
-                for p in per_rank[r]:
-                    n = p.numel()
-                    dst.append(p.data)
-                    src.append(recv[off : off + n].view_as(p))
-                    received.append(p)
-                    off += n
-            if dst:
-                torch._foreach_copy_(dst, src)
-            if self._shadows and received:
-                # .data copies do not bump p._version: re-cast the shadows explicitly
-                from ..models.fused import refresh_bf16_shadows
+        gloo = dist.get_backend(self.process_group) == "gloo"
+        for f in self._flats:
+            flat, smax = f["flat"], f["smax"]
+            own = flat[self.rank * smax : (self.rank + 1) * smax]
+            if gloo:  # gloo wants distinct input/output buffers and cannot overlap anyway
+                if flat.is_cuda:
+                    full = torch.empty(flat.numel(), dtype=flat.dtype)
+                    dist.all_gather_into_tensor(full, own.cpu(), group=self.process_group)
+                    flat.copy_(full)
+                else:
+                    dist.all_gather_into_tensor(flat, own.clone(), group=self.process_group)
+                self._after_gather(f)
+            else:
+                self._pending.append((dist.all_gather_into_tensor(flat, own, group=self.process_group, async_op=True), f))
+        for p in getattr(self, "_late", []):  # parameters added after construction: per-tensor broadcast
+            dist.broadcast(p.data, src=self.param_to_rank[id(p)], group=self.process_group)
+        if not self._attached:
+            self.wait_parameters()
 
-                refresh_bf16_shadows(received)
+    def wait_parameters(self) -> None:
+        """Make the current stream wait for the in-flight parameter all-gathers (no host block on
+        RCCL), then refresh the gathered regions' bf16 shadows."""
+        pend, self._pending = self._pending, []
+        for work, f in pend:
+            work.wait()
+            self._after_gather(f)
+
+    def _after_gather(self, f: dict) -> None:
+        if not self._shadows:
+            return
+        # .data copies do not bump p._version: re-cast the received parameters' shadows explicitly
+        from ..models.fused import refresh_bf16_shadows
+
+        mine = {id(p) for p in f["mine"]}
+        refresh_bf16_shadows([p for p in f["params"] if id(p) not in mine])
 
     # ------------------------------------------------------------------------------------------
     def state_dict(self):

@@ -19,9 +19,11 @@ all-reduce into its two halves and puts the optimizer in between:
   for exactly the buckets its parameters live in (a stream dependency on RCCL, not a host wait),
   then refreshes that bucket's bf16 compute shadows with one cast.
 
-Per step each rank moves the same bytes as an all-reduce (reduce-scatter + all-gather = 2·(W-1)/W
-of the gradient bytes), but the optimizer pass is 1/W as long and the parameter half of the traffic
-runs under the forward instead of the backward, which is where the xGMI links are otherwise idle.
+Per step each rank moves (W-1)/W of the fp32 gradient bytes (reduce-scatter) plus (W-1)/W of the
+*bf16* parameter bytes (all-gather of the compute shadows, ``gather_dtype="auto"`` with
+``bf16_shadows``): 6 B/param instead of an all-reduce's 8, the optimizer pass is 1/W as long, and
+the parameter half of the traffic runs under the forward instead of the backward, where the xGMI
+links are otherwise idle.
 Buckets are padded to a multiple of W elements (pad elements stay zero through AdamW).
 """
 
@@ -40,10 +42,11 @@ from .ddp import DEFAULT_BUCKET_MB, _unique_params, bucket_params
 
 class _ZBucket:
     __slots__ = ("idx", "params", "pbuf", "gbuf", "sbuf", "shard", "gshard", "master", "staged", "pending",
-                 "launched", "rs", "ag")
+                 "launched", "rs", "ag", "bf16")
 
-    def __init__(self, idx, params, pbuf, gbuf, sbuf, shard, gshard, master, staged):
+    def __init__(self, idx, params, pbuf, gbuf, sbuf, shard, gshard, master, staged, bf16=False):
         self.idx, self.params, self.pbuf, self.gbuf, self.sbuf = idx, params, pbuf, gbuf, sbuf
+        self.bf16 = bf16  # the parameter all-gather moves the bf16 compute shadows, not fp32 masters
         self.shard, self.gshard, self.master = shard, gshard, master
         self.staged = staged  # gloo + GPU tensors: collectives go through host copies
         self.pending = len(params)
@@ -94,6 +97,7 @@ class ZeroDDP(nn.Module):
         weight_decay: float = 0.01,
         bf16_shadows: bool = False,
         overlap_param_gather: bool = True,
+        gather_dtype: str = "auto",
         _collectives_at_world1: bool = False,
     ):
         super().__init__()
@@ -117,8 +121,27 @@ class ZeroDDP(nn.Module):
         self.buckets: list[_ZBucket] = []
         self._param_bucket: dict[nn.Parameter, _ZBucket] = {}
         self._views: dict[nn.Parameter, torch.Tensor] = {}
+        # bf16 parameter gather: the forward of the projection weights reads only their bf16 shadows,
+        # so only those go over the links (2 B/param instead of 4). Parameters read in fp32 by the
+        # forward (embedding, norm gains) get buckets of their own, gathered in fp32, placed LAST in
+        # the index order (their gradients complete last, and collectives are issued in index order).
+        # The other ranks' fp32 masters of a bf16 bucket go stale; wait_for_params()/state_dict()
+        # gather them on demand (checkpoints).
+        if gather_dtype not in ("auto", "bf16", "fp32"):
+            raise ValueError(f"gather_dtype must be auto|bf16|fp32, got {gather_dtype!r}")
+        self._bf16_gather = bf16_shadows and not self._solo and gather_dtype in ("auto", "bf16")
+        if self._bf16_gather:
+            from ..models.transformer import Linear as _Linear
+
+            lin = {id(m.weight) for m in module.modules() if isinstance(m, _Linear)}
+            a = [p for p in params if id(p) in lin and p.dim() == 2]
+            rest = [p for p in params if not (id(p) in lin and p.dim() == 2)]
+            groups = [(ps, True) for ps in bucket_params(a, cap)] + [(ps, False) for ps in bucket_params(rest, cap)]
+        else:
+            groups = [(ps, False) for ps in bucket_params(params, cap)]
+        self._masters_stale = False
         with torch.no_grad():
-            for i, ps in enumerate(bucket_params(params, cap)):
+            for i, (ps, b16) in enumerate(groups):
                 n = sum(p.numel() for p in ps)
                 shard = (n + W - 1) // W
                 dev = ps[0].device
@@ -143,7 +166,9 @@ class ZeroDDP(nn.Module):
                 master.grad = gshard
                 if self._solo and sbuf is not None:
                     setattr(master, _SHADOW, sbuf)
-                b = _ZBucket(i, ps, pbuf, gbuf, sbuf, shard, gshard, master, self._gloo and dev.type == "cuda")
+                elif b16:  # the update kernel writes this rank's shadow slice; the gather ships it
+                    setattr(master, _SHADOW, sbuf[r * shard : (r + 1) * shard])
+                b = _ZBucket(i, ps, pbuf, gbuf, sbuf, shard, gshard, master, self._gloo and dev.type == "cuda", b16)
                 self.buckets.append(b)
                 for p in ps:
                     self._param_bucket[p] = b
@@ -277,18 +302,39 @@ class ZeroDDP(nn.Module):
             return
         for b in reversed(self.buckets):  # forward order: the last buckets hold the first layers
             with annotate(f"comm.ag{b.idx}"):
-                if b.staged:
-                    full = torch.empty(b.pbuf.numel(), dtype=torch.float32)
-                    dist.all_gather_into_tensor(full, b.master.detach().cpu(), group=self.process_group)
-                    b.pbuf.copy_(full)
-                    b.ag = True
-                elif self._gloo:  # CPU: gloo wants a separate input buffer
-                    b.ag = dist.all_gather_into_tensor(b.pbuf, b.master.detach().clone(), group=self.process_group,
-                                                       async_op=True)
-                else:  # RCCL gathers in place: the input is this rank's slice of the output buffer
-                    b.ag = dist.all_gather_into_tensor(b.pbuf, b.master.detach(), group=self.process_group, async_op=True)
+                b.ag = self._gather(b.sbuf if b.bf16 else b.pbuf, b.shard, async_op=True)
+        self._masters_stale = self._masters_stale or any(b.bf16 for b in self.buckets)
         if not self.overlap_param_gather:
             self._wait_all_gathers()
+
+    def _gather(self, buf: torch.Tensor, shard: int, async_op: bool):
+        """All-gather this rank's slice of ``buf`` into all of ``buf``: the work handle, or True for
+        a completed host-staged gather (gloo cannot gather HIP tensors)."""
+        own = buf[self.rank * shard : (self.rank + 1) * shard]
+        if self._gloo and (buf.is_cuda or buf.dtype != torch.float32):
+            # (bf16 travels as fp32 through gloo: exact both ways)
+            full = torch.empty(buf.numel(), dtype=torch.float32)
+            dist.all_gather_into_tensor(full, own.float().cpu(), group=self.process_group)
+            buf.copy_(full)
+            return True
+        if self._gloo:  # CPU: gloo wants a separate input buffer
+            w = dist.all_gather_into_tensor(buf, own.clone(), group=self.process_group, async_op=async_op)
+        else:  # RCCL gathers in place: the input is this rank's slice of the output buffer
+            w = dist.all_gather_into_tensor(buf, own, group=self.process_group, async_op=async_op)
+        return w if async_op else True
+
+    @torch.no_grad()
+    def _gather_masters(self) -> None:
+        """Bring the other ranks' fp32 masters of the bf16-gathered buckets up to date (blocking)."""
+        if not self._masters_stale:
+            return
+        self._wait_all_gathers()
+        for b in self.buckets:
+            if b.bf16:
+                w = self._gather(b.pbuf, b.shard, async_op=True)
+                if w is not True:
+                    w.wait()
+        self._masters_stale = False
 
     def _wait_bucket(self, b: _ZBucket) -> None:
         if b.ag is None:
@@ -296,7 +342,10 @@ class ZeroDDP(nn.Module):
         if b.ag is not True:
             b.ag.wait()
         b.ag = None
-        if b.sbuf is not None:
+        if b.bf16:  # the gathered bytes ARE the shadows
+            for p in b.params:
+                mark_shadow_synced(p)
+        elif b.sbuf is not None:
             self._refresh_shadows(b)
 
     def _wait_buckets(self, ids) -> None:
@@ -315,14 +364,16 @@ class ZeroDDP(nn.Module):
                 mark_shadow_synced(p)
 
     def wait_for_params(self) -> None:
-        """Make the current stream wait for every pending parameter all-gather (before reading the
-        full parameters outside a forward, e.g. for a checkpoint)."""
+        """Make the current stream wait for every pending parameter all-gather and bring every fp32
+        master up to date (before reading the full parameters outside a forward, e.g. for a
+        checkpoint; with the bf16 gather this runs an fp32 all-gather of those buckets)."""
         self._wait_all_gathers()
+        self._gather_masters()
 
     def state_dict(self, *args, **kwargs):
-        self._wait_all_gathers()
+        self.wait_for_params()
         return self.module.state_dict(*args, **kwargs)
 
     def bucket_summary(self) -> list[dict]:
-        return [dict(bucket=b.idx, n_params=len(b.params), mb=b.pbuf.numel() * 4 / 2**20, shard=b.shard)
-                for b in self.buckets]
+        return [dict(bucket=b.idx, n_params=len(b.params), mb=b.pbuf.numel() * 4 / 2**20, shard=b.shard,
+                     gather="bf16" if b.bf16 else "fp32") for b in self.buckets]

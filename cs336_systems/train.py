@@ -192,6 +192,8 @@ def train(cfg: TrainConfig) -> dict:
             load_optimizer_state(path, opt, map_location=dev)
     else:
         ddp = model if use_graphs else wrap_ddp(model, cfg.ddp, bucket_size_mb=cfg.bucket_mb)
+    if isinstance(opt, ShardedOptimizer):
+        opt.attach(ddp)  # the in-place parameter all-gather is waited for by the next forward
     graphed = None
     batches = Batches(cfg, rank, world, dev)
     amp = dev.type == "cuda" and cfg.dtype == "bf16"
@@ -257,6 +259,8 @@ def train(cfg: TrainConfig) -> dict:
         if cfg.ckpt_dir and ((cfg.ckpt_every and done % cfg.ckpt_every == 0) or done == end):
             if zero:
                 ddp.wait_for_params()  # the parameter all-gathers of this step must land first
+            elif isinstance(opt, ShardedOptimizer):
+                opt.wait_parameters()
             # never let a diverged state become `latest` (keep-N would then prune the good ones):
             # this step's loss and the updated weights must be finite on every rank
             _check_finite_before_save(loss, model, done, dev)

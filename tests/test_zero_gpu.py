@@ -39,13 +39,18 @@ def _lm():
                                device=DEV, fused_layout=True)
 
 
-@pytest.mark.parametrize("collectives", [False, True])
-def test_zero_world1_matches_fused_adamw(rccl_world1, collectives):
-    """collectives=True also runs the RCCL reduce-scatter and the in-place all-gather + shadow cast."""
+@pytest.mark.parametrize("collectives,gather", [(False, "auto"), (True, "fp32"), (True, "bf16")])
+def test_zero_world1_matches_fused_adamw(rccl_world1, collectives, gather):
+    """collectives=True also runs the RCCL reduce-scatter and the in-place all-gather: of the fp32
+    masters + a shadow cast (gather fp32), or of the bf16 shadows the update kernel wrote, with the
+    fp32 masters gathered on demand by state_dict() (gather bf16)."""
     ref = _lm()
     ref_opt = ops.FusedAdamW(ref.parameters(), bf16_shadows=True, **OPT)
-    zero = ZeroDDP(_lm(), bucket_size_mb=2.0, bf16_shadows=True, _collectives_at_world1=collectives, **OPT)
+    zero = ZeroDDP(_lm(), bucket_size_mb=2.0, bf16_shadows=True, gather_dtype=gather,
+                   _collectives_at_world1=collectives, **OPT)
     assert len(zero.buckets) > 2
+    kinds = {b["gather"] for b in zero.bucket_summary()}
+    assert kinds == ({"bf16", "fp32"} if gather == "bf16" else {"fp32"})
     opt = zero.optimizer
     for it in range(3):
         x = torch.randint(0, 512, (4, 128), device=DEV, generator=torch.Generator(DEV).manual_seed(it))
