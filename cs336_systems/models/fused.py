@@ -33,6 +33,9 @@ from ..ops._ext import ops as _hip
 
 _SHADOW = "_cs336_bf16"
 _SHADOW_VER = "_cs336_bf16_ver"
+_SHADOW_GEN = "_cs336_bf16_gen"  # bumped on every shadow (re)write
+_SHADOW_T = "_cs336_bf16t"  # transposed bf16 shadow Wᵀ (d_in, d_out) view, written by the fused AdamW
+_SHADOW_T_GEN = "_cs336_bf16t_gen"  # shadow generation the Wᵀ was written at
 
 
 # ------------------------------------------------------------------------------------------
@@ -97,14 +100,42 @@ def get_shadow(p: torch.Tensor) -> torch.Tensor | None:
 
 def mark_shadow_synced(p: torch.Tensor) -> None:
     setattr(p, _SHADOW_VER, p._version)
+    setattr(p, _SHADOW_GEN, getattr(p, _SHADOW_GEN, 0) + 1)
+
+
+def get_shadow_t(p: torch.Tensor) -> torch.Tensor | None:
+    return getattr(p, _SHADOW_T, None)
+
+
+def mark_shadow_t_synced(p: torch.Tensor) -> None:
+    """Wᵀ holds the transpose of the CURRENT shadow (call right after mark_shadow_synced)."""
+    setattr(p, _SHADOW_T_GEN, getattr(p, _SHADOW_GEN, 0))
+
+
+def shadow_t_valid(p: torch.Tensor) -> bool:
+    """Wᵀ is usable iff the shadow is valid and Wᵀ was written with that very shadow generation
+    (any other shadow refresh -- a cast after a ZeRO gather, say -- bumps the generation)."""
+    return (
+        getattr(p, _SHADOW_T, None) is not None
+        and shadow_valid(p)
+        and getattr(p, _SHADOW_T_GEN, -1) == getattr(p, _SHADOW_GEN, 0)
+    )
 
 
 @torch.no_grad()
-def attach_bf16_shadows(module_or_params) -> int:
+def attach_bf16_shadows(module_or_params, transposed: bool | None = None) -> int:
     """Allocate bf16 shadows for every 2-D fp32 GPU weight (grouped weights get one contiguous
-    shadow per group, mirroring the master layout) and fill them. Returns #params."""
+    shadow per group, mirroring the master layout) and fill them. Returns #params.
+
+    ``transposed`` (default: ``CS336_WT`` != 0) also allocates Wᵀ shadows: each maximal run of
+    row-adjacent, equally wide weights of one storage (a fused QKV or W1|W3 group, or neighbours in
+    a ZeRO flat buffer) gets one (d_in, rows) bf16 tensor and every weight a column-block view of it,
+    so a group's Wᵀ is again one strided view. The fused AdamW rewrites them with the update
+    (``ops/adamw.py``), replacing the per-forward transpose of every weight."""
     src = module_or_params.parameters() if isinstance(module_or_params, nn.Module) else module_or_params
     params = [p for p in src if p.dim() == 2 and p.dtype == torch.float32 and p.is_cuda and not has_shadow(p)]
+    if transposed is None:
+        transposed = _transpose_weight()
     by_storage: dict[int, list[nn.Parameter]] = {}
     for p in params:
         by_storage.setdefault(p.untyped_storage().data_ptr(), []).append(p)
@@ -115,12 +146,37 @@ def attach_bf16_shadows(module_or_params) -> int:
         shadow_base = torch.empty(st_numel, dtype=torch.bfloat16, device=base.device)
         for p in group:
             setattr(p, _SHADOW, torch.as_strided(shadow_base, p.shape, p.stride(), p.storage_offset()))
-    refresh_bf16_shadows(params)
+        if transposed:
+            _attach_transposed(group)
+    refresh_bf16_shadows(params, transposed=True)
     return len(params)
 
 
+def _attach_transposed(group: list[nn.Parameter]) -> None:
+    """Wᵀ views for ``group`` (one storage, sorted by offset): one (d_in, rows) tensor per run."""
+    runs: list[list[nn.Parameter]] = []
+    for p in group:
+        if not p.is_contiguous() or p.shape[0] % 8 or p.shape[1] % 8:
+            continue
+        prev = runs[-1][-1] if runs else None
+        if prev is not None and prev.shape[1] == p.shape[1] and p.storage_offset() == prev.storage_offset() + prev.numel():
+            runs[-1].append(p)
+        else:
+            runs.append([p])
+    for run in runs:
+        d_in, rows = run[0].shape[1], sum(p.shape[0] for p in run)
+        wt = torch.empty(d_in, rows, dtype=torch.bfloat16, device=run[0].device)
+        off = 0
+        for p in run:
+            setattr(p, _SHADOW_T, wt[:, off : off + p.shape[0]])
+            off += p.shape[0]
+
+
 @torch.no_grad()
-def refresh_bf16_shadows(params) -> None:
+def refresh_bf16_shadows(params, transposed: bool = False) -> None:
+    """Re-cast the shadows of ``params`` from their fp32 masters (one multi-tensor launch); with
+    ``transposed`` also re-write their Wᵀ shadows (one transpose per weight: attach time only --
+    elsewhere a stale Wᵀ just makes the forward transpose the weight itself)."""
     ps = [p for p in params if has_shadow(p)]
     if not ps:
         return
@@ -131,6 +187,38 @@ def refresh_bf16_shadows(params) -> None:
             get_shadow(p).copy_(p.data)
     for p in ps:
         mark_shadow_synced(p)
+        wt = get_shadow_t(p) if transposed else None
+        if wt is not None:
+            wt.copy_(get_shadow(p).t())
+            mark_shadow_t_synced(p)
+
+
+def _adjacent_cols(ts: list[torch.Tensor]) -> torch.Tensor | None:
+    """If ``ts`` are column-adjacent blocks (unit column stride) of one storage, the combined view."""
+    t0 = ts[0]
+    if t0.dim() != 2 or t0.stride(1) != 1:
+        return None
+    ld, off, cols = t0.stride(0), t0.storage_offset(), 0
+    ptr = t0.untyped_storage().data_ptr()
+    for t in ts:
+        if (
+            t.dim() != 2
+            or t.shape[0] != t0.shape[0]
+            or t.stride() != (ld, 1)
+            or t.untyped_storage().data_ptr() != ptr
+            or t.storage_offset() != off + cols
+        ):
+            return None
+        cols += t.shape[1]
+    return torch.as_strided(t0, (t0.shape[0], cols), (ld, 1), off)
+
+
+def compute_weight_t(params: list[nn.Parameter]) -> torch.Tensor | None:
+    """The (d_in, rows) bf16 Wᵀ of a group (or single) of params from their transposed shadows,
+    or None when any is missing/stale (the caller transposes the compute weight instead)."""
+    if not all(shadow_t_valid(p) for p in params):
+        return None
+    return _adjacent_cols([get_shadow_t(p) for p in params])
 
 
 def compute_weight(params: list[nn.Parameter], dtype: torch.dtype) -> torch.Tensor:
@@ -278,7 +366,10 @@ class FusedLinearFn(torch.autograd.Function):
         # Wᵀ is made on the side stream right here, off the forward's critical path.
         ctx.wt_event = None
         ctx.w_t = x2.is_cuda and ctx.needs_input_grad[0] and w.dtype == torch.bfloat16 and _transpose_weight()
-        if ctx.w_t and torch.cuda.is_current_stream_capturing():
+        wt_shadow = compute_weight_t(list(weights)) if ctx.w_t else None
+        if wt_shadow is not None:  # Wᵀ written by the fused AdamW together with the bf16 shadow
+            w_saved = wt_shadow
+        elif ctx.w_t and torch.cuda.is_current_stream_capturing():
             w_saved = _transpose(w)  # inside a HIP-graph capture: stay on the capturing stream
         elif ctx.w_t:
             main = torch.cuda.current_stream(x2.device)

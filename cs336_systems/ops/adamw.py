@@ -48,6 +48,30 @@ def adamw_ref_(p, g, m, v, lr, beta1, beta2, eps, wd, t):
     p.sub_(lr * wd * p)
 
 
+def _wt_ok(p: torch.Tensor, state: dict, wt: torch.Tensor) -> bool:
+    """adamw_step_t's layout contract (csrc/bindings.cpp): contiguous 2-D fp32 tensors, R and C
+    multiples of 8, 16-B aligned pointers, Wᵀ a (C, R) view with unit column stride."""
+    from ..models.fused import get_shadow
+
+    g = p.grad
+
+    def al(t):
+        return t.data_ptr() % 16 == 0
+
+    return (
+        p.dim() == 2
+        and p.dtype == torch.float32
+        and p.shape[0] % 8 == 0
+        and p.shape[1] % 8 == 0
+        and p.is_contiguous()
+        and g.is_contiguous()
+        and wt.shape == (p.shape[1], p.shape[0])
+        and wt.stride(1) == 1
+        and wt.stride(0) % 8 == 0
+        and al(p) and al(g) and al(state["m"]) and al(state["v"]) and al(wt) and al(get_shadow(p))
+    )
+
+
 class _Overlap:
     """Bookkeeping of the backward-overlapped update (see the module docstring)."""
 
@@ -104,12 +128,16 @@ class FusedAdamW(torch.optim.Optimizer):
     # update launches
     # ------------------------------------------------------------------------------------------
     def _update(self, items: list[tuple[dict, torch.nn.Parameter]]) -> None:
-        """Update ``(group, param)`` pairs whose ``.grad`` is set, on the current stream."""
-        from ..models.fused import get_shadow, mark_shadow_synced
+        """Update ``(group, param)`` pairs whose ``.grad`` is set, on the current stream.
 
-        # bucket by (group, device, dtype, t, shadow) so each launch has one set of
-        # hyper-parameters, one bias correction and an all-or-nothing shadow list
-        buckets: dict[tuple, tuple[dict, list, list, list, list, list]] = {}
+        Weights with a transposed bf16 shadow (``models/fused.py``) go through ``adamw_step_t``,
+        which also writes Wᵀ in the same pass (+2 B/param instead of a 4 B/param transpose of every
+        weight in the next forward); the rest through the 1-D ``adamw_step``."""
+        from ..models.fused import get_shadow, get_shadow_t, mark_shadow_synced, mark_shadow_t_synced
+
+        # bucket by (group, device, dtype, t, shadow, Wᵀ) so each launch has one set of
+        # hyper-parameters, one bias correction and all-or-nothing shadow lists
+        buckets: dict[tuple, tuple[dict, list, list, list, list, list, list]] = {}
         for group, p in items:
             if p.grad.is_sparse:
                 raise RuntimeError("AdamW does not support sparse gradients")
@@ -119,27 +147,39 @@ class FusedAdamW(torch.optim.Optimizer):
                 state["v"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 state["t"] = 1
             sh = get_shadow(p)
-            key = (id(group), p.device, p.dtype, p.grad.dtype, state["t"], sh is not None)
-            b = buckets.setdefault(key, (group, [], [], [], [], []))
+            wt = get_shadow_t(p) if sh is not None else None
+            if wt is not None and not _wt_ok(p, state, wt):
+                wt = None
+            key = (id(group), p.device, p.dtype, p.grad.dtype, state["t"], sh is not None, wt is not None)
+            b = buckets.setdefault(key, (group, [], [], [], [], [], []))
             b[1].append(p)
             b[2].append(p.grad)
             b[3].append(state["m"])
             b[4].append(state["v"])
             if sh is not None:
                 b[5].append(sh)
+            if wt is not None:
+                b[6].append(wt)
             state["t"] += 1
-        for key, (group, ps, gs, ms, vs, ss) in buckets.items():
+        for key, (group, ps, gs, ms, vs, ss, wts) in buckets.items():
             t = key[4]
             lr, (beta1, beta2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
-            if use_hip(ps[0]) and all(x.is_contiguous() for x in ps + gs + ms + vs + ss):
+            hip = use_hip(ps[0]) and all(x.is_contiguous() for x in ps + gs + ms + vs + ss)
+            if hip and wts:
+                ops().adamw_step_t(ps, gs, ms, vs, ss, wts, lr, beta1, beta2, eps, wd, t)
+            elif hip:
                 ops().adamw_step(ps, gs, ms, vs, ss, lr, beta1, beta2, eps, wd, t)
             else:
                 for p, g, m, v in zip(ps, gs, ms, vs):
                     adamw_ref_(p, g.to(p.dtype), m, v, lr, beta1, beta2, eps, wd, t)
                 for p, s in zip(ps, ss):
                     s.copy_(p)
+                for p, w in zip(ps, wts):
+                    w.copy_(get_shadow(p).t())
             for p in ps if ss else ():
                 mark_shadow_synced(p)
+            for p in ps if wts else ():
+                mark_shadow_t_synced(p)
 
     @torch.no_grad()
     def step(self, closure: Callable | None = None):

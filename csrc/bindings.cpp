@@ -598,6 +598,60 @@ void adamw_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, s
                     (float)(1.0 - beta2), (float)eps, (float)(lr * weight_decay), (float)alpha_t, stream());
 }
 
+// AdamW over 2-D weights that also writes each weight's transposed bf16 shadow (Wᵀ, a (C, R) view
+// with unit column stride whose row stride may exceed R: a column block of a grouped Wᵀ)
+void adamw_step_t(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> exp_avg,
+                  std::vector<at::Tensor> exp_avg_sq, std::vector<at::Tensor> shadows, std::vector<at::Tensor> wts,
+                  double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step) {
+  const int n = (int)params.size();
+  if (n == 0) return;
+  TORCH_CHECK((int)grads.size() == n && (int)exp_avg.size() == n && (int)exp_avg_sq.size() == n &&
+                  (int)shadows.size() == n && (int)wts.size() == n,
+              "cs336: adamw_step_t list lengths differ");
+  check_same_dtype(params, at::kFloat, "params (fp32 master weights)");
+  check_same_dtype(exp_avg, at::kFloat, "exp_avg");
+  check_same_dtype(exp_avg_sq, at::kFloat, "exp_avg_sq");
+  check_same_dtype(shadows, at::kBFloat16, "bf16 shadows");
+  check_same_dtype(wts, at::kBFloat16, "transposed bf16 shadows");
+  const at::ScalarType gt = grads[0].scalar_type();
+  check_same_dtype(grads, gt, "grads");
+  const int64_t len = (int64_t)n * 6 + (n + 1) + (int64_t)n * 3;
+  at::Tensor host = at::empty({len}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+  int64_t* h = host.data_ptr<int64_t>();
+  int64_t tiles = 0;
+  auto aligned = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
+  for (int i = 0; i < n; ++i) {
+    const at::Tensor &p = params[i], &g = grads[i], &m = exp_avg[i], &v = exp_avg_sq[i], &s = shadows[i], &w = wts[i];
+    TORCH_CHECK(p.dim() == 2 && p.is_cuda() && p.is_contiguous() && g.is_contiguous() && m.is_contiguous() &&
+                    v.is_contiguous() && s.is_contiguous(),
+                "cs336: adamw_step_t needs contiguous 2-D GPU tensors");
+    const int64_t R = p.size(0), C = p.size(1);
+    TORCH_CHECK(g.sizes() == p.sizes() && m.sizes() == p.sizes() && v.sizes() == p.sizes() && s.sizes() == p.sizes(),
+                "cs336: adamw_step_t shape mismatch");
+    TORCH_CHECK(w.dim() == 2 && w.size(0) == C && w.size(1) == R && w.stride(1) == 1 && w.stride(0) % 8 == 0,
+                "cs336: Wᵀ must be a (C, R) view with unit column stride and a row stride multiple of 8");
+    TORCH_CHECK(R % 8 == 0 && C % 8 == 0, "cs336: adamw_step_t needs R, C multiples of 8");
+    TORCH_CHECK(aligned(p) && aligned(g) && aligned(m) && aligned(v) && aligned(s) && aligned(w),
+                "cs336: adamw_step_t pointers must be 16-byte aligned");
+    const at::Tensor* ts[6] = {&p, &g, &m, &v, &s, &w};
+    for (int k = 0; k < 6; ++k) h[(int64_t)i * 6 + k] = reinterpret_cast<int64_t>(ts[k]->data_ptr());
+    h[(int64_t)n * 6 + i] = tiles;
+    tiles += ((R + 255) / 256) * ((C + 63) / 64);
+    int64_t* d = h + (int64_t)n * 6 + (n + 1) + 3 * i;
+    d[0] = R;
+    d[1] = C;
+    d[2] = w.stride(0);
+  }
+  h[(int64_t)n * 6 + n] = tiles;
+  c10::DeviceGuard guard(params[0].device());
+  at::Tensor dev = host.to(params[0].device(), /*non_blocking=*/true);
+  const int64_t* dptr = dev.data_ptr<int64_t>();
+  const double alpha_t = lr * (std::sqrt(1.0 - std::pow(beta2, (double)step)) / (1.0 - std::pow(beta1, (double)step)));
+  cs336::adamw_step_t(dptr, dptr + (int64_t)n * 6, dptr + (int64_t)n * 6 + (n + 1), n, tiles, to_dtype(grads[0]),
+                      (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
+                      (float)(lr * weight_decay), (float)alpha_t, stream());
+}
+
 void multi_tensor_cast_bf16(std::vector<at::Tensor> src, std::vector<at::Tensor> dst) {
   if (src.empty()) return;
   check_same_dtype(src, at::kFloat, "src");
@@ -675,6 +729,10 @@ TORCH_LIBRARY(cs336, m) {
       "adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, "
       "Tensor(d!)[] shadows, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("multi_tensor_l2norm(Tensor[] tensors) -> Tensor");
+  m.def(
+      "adamw_step_t(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, "
+      "Tensor(d!)[] shadows, Tensor(e!)[] wts, float lr, float beta1, float beta2, float eps, float weight_decay, "
+      "int step) -> ()");
   m.def("occupy(int n_workgroups, int lds_bytes, float ms, Tensor(a!) counter) -> ()");
   m.def("multi_tensor_scale_(Tensor(a!)[] tensors, Tensor scale) -> ()");
 }
@@ -700,6 +758,7 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("xent_fwd", &xent_fwd);
   m.impl("xent_bwd", &xent_bwd);
   m.impl("adamw_step", &adamw_step);
+  m.impl("adamw_step_t", &adamw_step_t);
   m.impl("multi_tensor_l2norm", &multi_tensor_l2norm);
   m.impl("occupy", &occupy);
   m.impl("multi_tensor_scale_", &multi_tensor_scale_);

@@ -90,6 +90,12 @@ constexpr int64_t kMTChunk = 32768;  // elements per workgroup chunk
 // table pointers per tensor: p, g, m, v (+ bf16 shadow when shadow == true)
 void adamw_step(const TensorTable& tt, DType grad_t, bool shadow, float beta1, float beta2, float one_minus_beta1,
                 float one_minus_beta2, float eps, float lr_wd, float alpha_t, hipStream_t s);
+// 2-D weights, also writing the transposed bf16 shadow: per tensor 6 pointers (p, g, m, v, shadow,
+// Wᵀ at its first element) and dims (R, C, ldt); tiles of 256 rows x 64 columns; R, C multiples of 8,
+// every pointer 16-B aligned, ldt a multiple of 8 (host checks)
+void adamw_step_t(const int64_t* ptrs, const int64_t* tile_base, const int64_t* dims, int n, int64_t total_tiles,
+                  DType grad_t, float beta1, float beta2, float one_minus_beta1, float one_minus_beta2, float eps,
+                  float lr_wd, float alpha_t, hipStream_t s);
 // table pointers per tensor: fp32 src, bf16 dst
 void multi_tensor_cast_bf16(const TensorTable& tt, hipStream_t s);
 void multi_tensor_sumsq(const TensorTable& tt, DType t, float* partials, hipStream_t s);

@@ -91,6 +91,74 @@ __global__ __launch_bounds__(256) void adamw_kernel(const int64_t* __restrict__ 
     }
   }
 }
+
+// ---- AdamW + transposed bf16 shadow --------------------------------------------------------------
+// For 2-D weights (R x C, row-major) the update also writes Wᵀ in bf16 (C x R view with row stride
+// ldt), the K-major operand of the input-gradient GEMM (models/fused.py), so the forward needs no
+// per-call transpose of every weight. One workgroup = 256 rows x 64 columns; each thread updates an
+// 8 x 8 block row by row (8 x 32-B row segments per tensor: a wave's loads cover 8 rows x 256 B),
+// keeps the 8 x 8 bf16 results packed in 32 VGPRs, and writes them transposed as eight 16-B column
+// chunks (a wave's stores cover 8 output rows x 128 B). Same update arithmetic as adamw_kernel.
+__device__ __forceinline__ uint32_t lo_pair(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
+__device__ __forceinline__ uint32_t hi_pair(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
+
+template <typename TG>
+__global__ __launch_bounds__(256) void adamw_t_kernel(const int64_t* __restrict__ ptrs,
+                                                      const int64_t* __restrict__ tile_base,
+                                                      const int64_t* __restrict__ dims, int n, float b1, float b2,
+                                                      float omb1, float omb2, float eps, float lr_wd, float alpha_t) {
+  const int64_t tile = blockIdx.x;
+  const int t = find_tensor(tile_base, n, tile);
+  float* p = reinterpret_cast<float*>(ptrs[6 * t + 0]);
+  const auto* g = reinterpret_cast<const typename Elem<TG>::storage*>(ptrs[6 * t + 1]);
+  float* m = reinterpret_cast<float*>(ptrs[6 * t + 2]);
+  float* v = reinterpret_cast<float*>(ptrs[6 * t + 3]);
+  bf16_t* sh = reinterpret_cast<bf16_t*>(ptrs[6 * t + 4]);
+  bf16_t* wt = reinterpret_cast<bf16_t*>(ptrs[6 * t + 5]);
+  const int64_t R = dims[3 * t], C = dims[3 * t + 1], ldt = dims[3 * t + 2];
+  const int64_t ctiles = (C + 63) >> 6;
+  const int64_t local = tile - tile_base[t];
+  const int ch = threadIdx.x & 7, rr = threadIdx.x >> 3;
+  const int64_t r = (local / ctiles) * 256 + 8 * rr;  // first of this thread's 8 rows
+  const int64_t c = (local % ctiles) * 64 + 8 * ch;   // first of its 8 columns
+  if (r >= R || c >= C) return;                       // R, C multiples of 8 (host check)
+  uint32_t w[8][4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t i = (r + j) * C + c;
+    float4 p0 = *reinterpret_cast<float4*>(p + i), p1 = *reinterpret_cast<float4*>(p + i + 4);
+    float4 m0 = *reinterpret_cast<float4*>(m + i), m1 = *reinterpret_cast<float4*>(m + i + 4);
+    float4 v0 = *reinterpret_cast<float4*>(v + i), v1 = *reinterpret_cast<float4*>(v + i + 4);
+    const float4 g0 = load4<TG>(g + i), g1 = load4<TG>(g + i + 4);
+    adamw_elem(p0.x, g0.x, m0.x, v0.x, b1, omb1, b2, omb2, eps, alpha_t, lr_wd);
+    adamw_elem(p0.y, g0.y, m0.y, v0.y, b1, omb1, b2, omb2, eps, alpha_t, lr_wd);
+    adamw_elem(p0.z, g0.z, m0.z, v0.z, b1, omb1, b2, omb2, eps, alpha_t, lr_wd);
+    adamw_elem(p0.w, g0.w, m0.w, v0.w, b1, omb1, b2, omb2, eps, alpha_t, lr_wd);
+    adamw_elem(p1.x, g1.x, m1.x, v1.x, b1, omb1, b2, omb2, eps, alpha_t, lr_wd);
+    adamw_elem(p1.y, g1.y, m1.y, v1.y, b1, omb1, b2, omb2, eps, alpha_t, lr_wd);
+    adamw_elem(p1.z, g1.z, m1.z, v1.z, b1, omb1, b2, omb2, eps, alpha_t, lr_wd);
+    adamw_elem(p1.w, g1.w, m1.w, v1.w, b1, omb1, b2, omb2, eps, alpha_t, lr_wd);
+    *reinterpret_cast<float4*>(p + i) = p0;
+    *reinterpret_cast<float4*>(p + i + 4) = p1;
+    *reinterpret_cast<float4*>(m + i) = m0;
+    *reinterpret_cast<float4*>(m + i + 4) = m1;
+    *reinterpret_cast<float4*>(v + i) = v0;
+    *reinterpret_cast<float4*>(v + i + 4) = v1;
+    w[j][0] = (uint32_t)f32_to_bf16(p0.x) | ((uint32_t)f32_to_bf16(p0.y) << 16);
+    w[j][1] = (uint32_t)f32_to_bf16(p0.z) | ((uint32_t)f32_to_bf16(p0.w) << 16);
+    w[j][2] = (uint32_t)f32_to_bf16(p1.x) | ((uint32_t)f32_to_bf16(p1.y) << 16);
+    w[j][3] = (uint32_t)f32_to_bf16(p1.z) | ((uint32_t)f32_to_bf16(p1.w) << 16);
+    *reinterpret_cast<uint4*>(sh + i) = make_uint4(w[j][0], w[j][1], w[j][2], w[j][3]);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {  // Wᵀ row c + k holds column c + k of the block; element k sits in dword k/2
+    const int d = k >> 1;
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = (k & 1) ? hi_pair(w[2 * q][d], w[2 * q + 1][d]) : lo_pair(w[2 * q][d], w[2 * q + 1][d]);
+    *reinterpret_cast<uint4*>(wt + (c + k) * ldt + r) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
 #pragma clang fp contract(on)
 
 // ---- sum of squares (per-chunk partials, deterministic) ----------------------------------------
@@ -172,6 +240,23 @@ void adamw_step(const TensorTable& tt, DType grad_t, bool shadow, float beta1, f
     case DType::F32: by_shadow(float{}); break;
     case DType::BF16: by_shadow(BF16{}); break;
     case DType::F16: by_shadow(F16{}); break;
+  }
+}
+
+void adamw_step_t(const int64_t* ptrs, const int64_t* tile_base, const int64_t* dims, int n, int64_t total_tiles,
+                  DType grad_t, float beta1, float beta2, float one_minus_beta1, float one_minus_beta2, float eps,
+                  float lr_wd, float alpha_t, hipStream_t s) {
+  if (total_tiles == 0) return;
+  const dim3 grid((unsigned)total_tiles), block(256);
+  auto go = [&](auto tg) {
+    using TG = decltype(tg);
+    hipLaunchKernelGGL((adamw_t_kernel<TG>), grid, block, 0, s, ptrs, tile_base, dims, n, beta1, beta2,
+                       one_minus_beta1, one_minus_beta2, eps, lr_wd, alpha_t);
+  };
+  switch (grad_t) {
+    case DType::F32: go(float{}); break;
+    case DType::BF16: go(BF16{}); break;
+    case DType::F16: go(F16{}); break;
   }
 }
 
