@@ -18,6 +18,7 @@ OPT = dict(lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
 @pytest.mark.parametrize("shape", [(1600, 1600), (10000, 1600), (1600, 6400), (264, 72)])
 @pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
 def test_adamw_t_matches_adamw(shape, gdt):
+    assert ops.load_ext(), ops.load_error()
     torch.manual_seed(0)
     p = torch.randn(*shape, device=DEV)
     g = torch.randn(*shape, device=DEV).to(gdt)
