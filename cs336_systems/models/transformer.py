@@ -219,8 +219,11 @@ class CausalMultiHeadSelfAttention(nn.Module):
     def _fused_path(self, x3, pos, B, N):
         """GPU path over the grouped QKV weight: one GEMM -> RoPE + FA2 on strided views -> o."""
         w = [self.q_proj.weight, self.k_proj.weight, self.v_proj.weight]
-        if _ATTN_IMPL == "naive" or not ops.use_hip(x3) or self.d_k not in (32, 64, 128):
+        if _ATTN_IMPL == "naive" or not ops.use_hip(x3) or self.d_k not in (32, 64, 80, 128):
             return None
+        cdt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x3.dtype
+        if self.d_k == 80 and cdt not in (torch.bfloat16, torch.float16):
+            return None  # d_head 80 is native for 16-bit only; fp32 takes the padded FA2 path below
         if fused.grouped_view(w) is None:
             return None
         p = _normalize_pos(pos, B, N)

@@ -147,7 +147,11 @@ def _pad_d(x, Dp):
     return torch.nn.functional.pad(x, (0, Dp - D))
 
 
-def _padded_d(D):
+def _padded_d(D, dtype=None):
+    """Head dim the kernels run at: 32/64/128 natively, 80 natively for 16-bit inputs (computed
+    as 96 inside the kernel, no copies); anything else is zero-padded on the host."""
+    if D == 80 and dtype in (torch.bfloat16, torch.float16):
+        return 80
     for s in _SUPPORTED_D:
         if D <= s:
             return s
@@ -158,7 +162,7 @@ def flash_attn_fwd(q, k, v, causal, scale):
     """Raw kernel call on 4-D (B,H,N,D) views (last dim contiguous). Returns O (B,H,N,D) in
     (B,N,H,D) memory order and LSE (B,H,Nq) fp32."""
     D = q.shape[-1]
-    Dp = _padded_d(D)
+    Dp = _padded_d(D, q.dtype)
     if Dp != D:
         o, lse = ops().fa_fwd(_pad_d(q, Dp), _pad_d(k, Dp), _pad_d(v, Dp), causal, scale)
         return o[..., :D], lse
@@ -168,7 +172,7 @@ def flash_attn_fwd(q, k, v, causal, scale):
 
 def flash_attn_bwd(do, q, k, v, o, lse, causal, scale):
     D = q.shape[-1]
-    Dp = _padded_d(D)
+    Dp = _padded_d(D, q.dtype)
     if Dp != D:
         dq, dk, dv = ops().fa_bwd(
             _pad_d(do, Dp), _pad_d(q, Dp), _pad_d(k, Dp), _pad_d(v, Dp), _pad_d(o, Dp), lse, causal, scale

@@ -30,14 +30,16 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   const AttnParams p = bp.f;  // by value: a reference would spill the kernarg struct to scratch
   constexpr bool F32 = std::is_same<T, float>::value;
   constexpr int ES = sizeof(S);
-  constexpr int RB = D * ES, CPR = RB / 16, EPC = 16 / ES;
+  constexpr int DP = PadD<D>::value;  // compute width (80 -> 96; d >= D is zero, never loaded/stored)
+  constexpr int RB = DP * ES, CPR = RB / 16, EPC = 16 / ES, CREAL = D * ES / 16;
   // D=128 streams 32-key tiles: halves the S^T/dP^T/staging registers so the kernel fits 256
   // VGPRs without spilling (64-key tiles spilled at occupancy 1)
-  constexpr int BM = 128, BN = D == 128 ? 32 : 64;
+  constexpr int BM = 128, BN = DP == 128 ? 32 : 64;
   constexpr int NT = BN / 32;
   constexpr int TILE = BN * RB;
   constexpr int LPT = BN * CPR / 256;
-  constexpr int NDT = D / 32;
+  static_assert(BN * CPR % 256 == 0, "staging rounds must be whole");
+  constexpr int NDT = DP / 32;
   constexpr bool PREFETCH = !(F32 && D == 128);
 
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
@@ -65,13 +67,13 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   const Rope rope{p.rope_cos, p.rope_sin, D / 2};
   const int64_t* rpos = p.rope_pos ? p.rope_pos + (int64_t)b * p.Nq : nullptr;
   const int64_t qpos = rpos && valid_q ? rpos[qrow] : qrow;
-  constexpr int NQF = F32 ? D / 8 : D / 16;
+  constexpr int NQF = F32 ? DP / 8 : DP / 16;
   uint4 qf[NQF], dof[NQF];
   float delta = 0.f;
 #pragma unroll
   for (int i = 0; i < NQF; ++i) {
-    const int e = F32 ? (hh * (D / 2) + 4 * i) : (16 * i + 8 * hh);
-    if (valid_q) {
+    const int e = F32 ? (hh * (DP / 2) + 4 * i) : (16 * i + 8 * hh);
+    if (valid_q && (DP == D || e < D)) {
       qf[i] = *reinterpret_cast<const uint4*>(Qp + (int64_t)qrow * p.q_sn + e);
       if (ROPE) qf[i] = rope_chunk<T>(qf[i], rope, qpos, e, 1.f);
       dof[i] = *reinterpret_cast<const uint4*>(dOp + (int64_t)qrow * bp.do_sn + e);
@@ -101,8 +103,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
       const int c = tid + 256 * i;
       const int r = c / CPR, ch = c % CPR;
       const int key = j * BN + r;
-      if (ROPE) kst_rc[i] = rope_coef<T>(rope, key < p.Nk ? (rpos ? rpos[key] : key) : 0, ch * EPC);
-      if (key < p.Nk) {
+      if (ROPE) kst_rc[i] = rope_coef<T>(rope, key < p.Nk ? (rpos ? rpos[key] : key) : 0, ch < CREAL ? ch * EPC : 0);
+      if (key < p.Nk && (CREAL == CPR || ch < CREAL)) {
         kst[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)key * p.k_sn + ch * EPC);
         vst[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)key * p.v_sn + ch * EPC);
       } else {
@@ -148,9 +150,9 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
         dp[t] = zero16();
         if constexpr (F32) {
 #pragma unroll
-          for (int i = 0; i < D / 8; ++i) {
-            const float4 kv = lds_f4<RB>(Ks, 32 * t + l32, hh * (D / 2) + 4 * i);
-            const float4 vv = lds_f4<RB>(Vs, 32 * t + l32, hh * (D / 2) + 4 * i);
+          for (int i = 0; i < DP / 8; ++i) {
+            const float4 kv = lds_f4<RB>(Ks, 32 * t + l32, hh * (DP / 2) + 4 * i);
+            const float4 vv = lds_f4<RB>(Vs, 32 * t + l32, hh * (DP / 2) + 4 * i);
             const float4 qv = __builtin_bit_cast(float4, qf[i]);
             const float4 gv = __builtin_bit_cast(float4, dof[i]);
             s[t] = mma_f32(kv.x, qv.x, s[t]);
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
           }
         } else {
 #pragma unroll
-          for (int ks = 0; ks < D / 16; ++ks) {
+          for (int ks = 0; ks < DP / 16; ++ks) {
             s[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Ks, 32 * t, ks, lane), as_frag<T>(qf[ks]), s[t]);
             dp[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Vs, 32 * t, ks, lane), as_frag<T>(dof[ks]), dp[t]);
           }
@@ -226,6 +228,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d = dt * 32 + 8 * g + 4 * hh;
+        if (DP != D && d >= D) continue;
         float v0 = dq[dt][4 * g] * sc, v1 = dq[dt][4 * g + 1] * sc, v2 = dq[dt][4 * g + 2] * sc,
               v3 = dq[dt][4 * g + 3] * sc;
         if (ROPE) rope_inv4(v0, v1, v2, v3, rope, qpos, d);  // dQ w.r.t. the un-rotated q
@@ -246,7 +249,8 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
   const AttnParams p = bp.f;  // by value: a reference would spill the kernarg struct to scratch
   constexpr bool F32 = std::is_same<T, float>::value;
   constexpr int ES = sizeof(S);
-  constexpr int RB = D * ES, CPR = RB / 16, EPC = 16 / ES;
+  constexpr int DP = PadD<D>::value;  // compute width (80 -> 96; d >= D is zero, never loaded/stored)
+  constexpr int RB = DP * ES, CPR = RB / 16, EPC = 16 / ES, CREAL = D * ES / 16;
   // 64-query tiles; at D=128 (one workgroup per CU anyway) part of the state lives in AGPRs
   // rather than halving the tile: 1153 -> 1046 us at N=4096 (fp32 keeps 32-query tiles)
   constexpr int BK = 128, BQ = (D == 128 && std::is_same<T, float>::value) ? 32 : 64;
@@ -254,7 +258,8 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
   constexpr int TILE = BQ * RB;
   constexpr int BUF = 2 * TILE + 2 * BQ * 4;  // Q, dO images + L2, delta rows
   constexpr int LPT = BQ * CPR / 256;
-  constexpr int NDT = D / 32;
+  static_assert(BQ * CPR % 256 == 0, "staging rounds must be whole");
+  constexpr int NDT = DP / 32;
   constexpr bool PREFETCH = !(F32 && D == 128);
 
   __shared__ __attribute__((aligned(16))) char smem[(PREFETCH ? 2 : 1) * BUF];
@@ -283,12 +288,12 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
   const Rope rope{p.rope_cos, p.rope_sin, D / 2};
   const int64_t* rpos = p.rope_pos ? p.rope_pos + (int64_t)b * p.Nq : nullptr;
   const int64_t kpos = rpos && valid_k ? rpos[krow] : krow;
-  constexpr int NKF = F32 ? D / 8 : D / 16;
+  constexpr int NKF = F32 ? DP / 8 : DP / 16;
   uint4 kf[NKF], vf[NKF];
 #pragma unroll
   for (int i = 0; i < NKF; ++i) {
-    const int e = F32 ? (hh * (D / 2) + 4 * i) : (16 * i + 8 * hh);
-    if (valid_k) {
+    const int e = F32 ? (hh * (DP / 2) + 4 * i) : (16 * i + 8 * hh);
+    if (valid_k && (DP == D || e < D)) {
       kf[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)krow * p.k_sn + e);
       if (ROPE) kf[i] = rope_chunk<T>(kf[i], rope, kpos, e, 1.f);
       vf[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)krow * p.v_sn + e);
@@ -310,8 +315,8 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
       const int c = tid + 256 * i;
       const int r = c / CPR, ch = c % CPR;
       const int q = qbase + r;
-      if (ROPE) qst_rc[i] = rope_coef<T>(rope, q < p.Nq ? (rpos ? rpos[q] : q) : 0, ch * EPC);
-      if (q < p.Nq) {
+      if (ROPE) qst_rc[i] = rope_coef<T>(rope, q < p.Nq ? (rpos ? rpos[q] : q) : 0, ch < CREAL ? ch * EPC : 0);
+      if (q < p.Nq && (CREAL == CPR || ch < CREAL)) {
         qst[i] = *reinterpret_cast<const uint4*>(Qp + (int64_t)q * p.q_sn + ch * EPC);
         dst[i] = *reinterpret_cast<const uint4*>(dOp + (int64_t)q * bp.do_sn + ch * EPC);
       } else {
@@ -371,9 +376,9 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
         dp[t] = zero16();
         if constexpr (F32) {
 #pragma unroll
-          for (int i = 0; i < D / 8; ++i) {
-            const float4 qv = lds_f4<RB>(Qs, 32 * t + l32, hh * (D / 2) + 4 * i);
-            const float4 gv = lds_f4<RB>(dOs, 32 * t + l32, hh * (D / 2) + 4 * i);
+          for (int i = 0; i < DP / 8; ++i) {
+            const float4 qv = lds_f4<RB>(Qs, 32 * t + l32, hh * (DP / 2) + 4 * i);
+            const float4 gv = lds_f4<RB>(dOs, 32 * t + l32, hh * (DP / 2) + 4 * i);
             const float4 kv = __builtin_bit_cast(float4, kf[i]);
             const float4 vv = __builtin_bit_cast(float4, vf[i]);
             s[t] = mma_f32(qv.x, kv.x, s[t]);
@@ -387,7 +392,7 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
           }
         } else {
 #pragma unroll
-          for (int ks = 0; ks < D / 16; ++ks) {
+          for (int ks = 0; ks < DP / 16; ++ks) {
             s[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Qs, 32 * t, ks, lane), as_frag<T>(kf[ks]), s[t]);
             dp[t] = Mma16<T>::mma(lds_row_frag<T, RB>(dOs, 32 * t, ks, lane), as_frag<T>(vf[ks]), dp[t]);
           }
@@ -465,6 +470,7 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d = dt * 32 + 8 * g + 4 * hh;
+        if (DP != D && d >= D) continue;
         float v0 = dk[dt][4 * g] * sc, v1 = dk[dt][4 * g + 1] * sc, v2 = dk[dt][4 * g + 2] * sc,
               v3 = dk[dt][4 * g + 3] * sc;
         if (ROPE) rope_inv4(v0, v1, v2, v3, rope, kpos, d);  // dK w.r.t. the un-rotated k
@@ -497,6 +503,14 @@ void launch_bwd_d(const AttnBwdParams& bp, hipStream_t s) {
   switch (bp.f.D) {
     case 32: launch_bwd<T, 32>(bp, s); break;
     case 64: launch_bwd<T, 64>(bp, s); break;
+    case 80:
+      if constexpr (std::is_same<T, float>::value) {
+        fprintf(stderr, "fa_bwd: head dim 80 is 16-bit only\n");
+        abort();
+      } else {
+        launch_bwd<T, 80>(bp, s);
+      }
+      break;
     case 128: launch_bwd<T, 128>(bp, s); break;
     default: fprintf(stderr, "fa_bwd: unsupported head dim %d\n", bp.f.D); abort();
   }

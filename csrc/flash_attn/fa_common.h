@@ -51,10 +51,25 @@ __device__ __forceinline__ f32x16 zero16() {
   return z;
 }
 
+// ---- padded head dims ------------------------------------------------------------------------
+// d_head 80 (the 2.7b model) runs as 96 = 3 x 32 inside the kernels: d 80..95 are zero in the LDS
+// images and fragments (zeros add nothing to S, dP or the d-sums) and never loaded or stored, so
+// there is no host-side padding copy and 20 % (not 60 %) extra MFMA work.
+template <int D>
+struct PadD {
+  static constexpr int value = D % 32 == 0 ? D : (D + 31) / 32 * 32;
+};
+
 // ---- swizzle: physical 16-B chunk = chunk ^ swz(row) --------------------------------------
 template <int RB>
 __device__ __forceinline__ int swz(int r) {
   if constexpr (RB == 64) {
+    return (r >> 2) & 3;
+  } else if constexpr (RB == 192) {
+    // 12-chunk rows (d_head 80 stored padded to 96): row r starts at slot 12r mod 16, so rows with the
+    // same r mod 4 share a slot pair; XOR-ing the chunk's low 2 bits with (r>>2)&3 spreads every
+    // ds_read_b128 lane group and every ds_read_b64_tr_b16 half over distinct banks (checked by
+    // enumeration of both access patterns); chunk groups of 4 stay inside the 12-chunk row
     return (r >> 2) & 3;
   } else if constexpr (RB == 128) {
     const int g = (r >> 1) & 7;

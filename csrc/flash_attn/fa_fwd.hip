@@ -24,13 +24,16 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
   typedef typename Elem<T>::storage S;
   constexpr bool F32 = std::is_same<T, float>::value;
   constexpr int ES = sizeof(S);
-  constexpr int RB = D * ES;       // bytes per row
+  constexpr int DP = PadD<D>::value;  // compute width (80 -> 96; d >= D is zero, never loaded/stored)
+  constexpr int RB = DP * ES;      // bytes per LDS row
   constexpr int CPR = RB / 16;     // 16-byte chunks per row
+  constexpr int CREAL = D * ES / 16;  // chunks that hold real data
   constexpr int EPC = 16 / ES;     // elements per chunk
   constexpr int BM = 128, BN = 64;
   constexpr int TILE = BN * RB;
   constexpr int LPT = BN * CPR / 256;  // 16-B staging loads per thread per tile
-  constexpr int NDT = D / 32;          // 32-wide d tiles of O^T
+  static_assert(BN * CPR % 256 == 0, "staging rounds must be whole");
+  constexpr int NDT = DP / 32;         // 32-wide d tiles of O^T
   constexpr bool PREFETCH = !(F32 && D == 128);
 
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
@@ -55,16 +58,17 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
   const bool valid_q = qrow < p.Nq;
 
   // ---- Q fragments (B operand), resident for the whole kernel -------------------------------
-  constexpr int NQF = F32 ? D / 8 : D / 16;  // uint4 per lane
+  constexpr int NQF = F32 ? DP / 8 : DP / 16;  // uint4 per lane
   const Rope rope{p.rope_cos, p.rope_sin, D / 2};
   const int64_t* rpos = p.rope_pos ? p.rope_pos + (int64_t)b * p.Nq : nullptr;
   uint4 qf[NQF];
 #pragma unroll
   for (int i = 0; i < NQF; ++i) {
     // 16-bit: chunk 2*ks + hh  |  f32: d = hh*D/2 + 4*i .. +3
-    const int e = F32 ? (hh * (D / 2) + 4 * i) : (16 * i + 8 * hh);
-    qf[i] = valid_q ? *reinterpret_cast<const uint4*>(Qp + (int64_t)qrow * p.q_sn + e) : make_uint4(0, 0, 0, 0);
-    if (ROPE && valid_q) qf[i] = rope_chunk<T>(qf[i], rope, rpos ? rpos[qrow] : qrow, e, 1.f);
+    const int e = F32 ? (hh * (DP / 2) + 4 * i) : (16 * i + 8 * hh);
+    const bool in = valid_q && e < D;
+    qf[i] = in ? *reinterpret_cast<const uint4*>(Qp + (int64_t)qrow * p.q_sn + e) : make_uint4(0, 0, 0, 0);
+    if (ROPE && in) qf[i] = rope_chunk<T>(qf[i], rope, rpos ? rpos[qrow] : qrow, e, 1.f);
   }
 
   const int kv_end = CAUSAL ? min(p.Nk, q0 + BM) : p.Nk;
@@ -78,8 +82,8 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
       const int c = tid + 256 * i;
       const int r = c / CPR, ch = c % CPR;
       const int key = j * BN + r;
-      if (ROPE) kst_rc[i] = rope_coef<T>(rope, key < p.Nk ? (rpos ? rpos[key] : key) : 0, ch * EPC);
-      if (key < p.Nk) {
+      if (ROPE) kst_rc[i] = rope_coef<T>(rope, key < p.Nk ? (rpos ? rpos[key] : key) : 0, ch < CREAL ? ch * EPC : 0);
+      if (key < p.Nk && (CREAL == CPR || ch < CREAL)) {
         kst[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)key * p.k_sn + ch * EPC);
         vst[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)key * p.v_sn + ch * EPC);
       } else {
@@ -127,8 +131,8 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
         s[t] = zero16();
         if constexpr (F32) {
 #pragma unroll
-          for (int i = 0; i < D / 8; ++i) {
-            const float4 kv = lds_f4<RB>(Ks, 32 * t + l32, hh * (D / 2) + 4 * i);
+          for (int i = 0; i < DP / 8; ++i) {
+            const float4 kv = lds_f4<RB>(Ks, 32 * t + l32, hh * (DP / 2) + 4 * i);
             const float4 qv = __builtin_bit_cast(float4, qf[i]);
             s[t] = mma_f32(kv.x, qv.x, s[t]);
             s[t] = mma_f32(kv.y, qv.y, s[t]);
@@ -137,7 +141,7 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
           }
         } else {
 #pragma unroll
-          for (int ks = 0; ks < D / 16; ++ks)
+          for (int ks = 0; ks < DP / 16; ++ks)
             s[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Ks, 32 * t, ks, lane), as_frag<T>(qf[ks]), s[t]);
         }
       }
@@ -227,8 +231,9 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d = dt * 32 + 8 * g + 4 * hh;
-        store4<T>(orow + d, make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
-                                        o[dt][4 * g + 3] * inv));
+        if (DP == D || d < D)
+          store4<T>(orow + d, make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
+                                          o[dt][4 * g + 3] * inv));
       }
     if (hh == 0) p.lse[((int64_t)b * p.H + h) * p.Nq + qrow] = l > 0.f ? (m + __log2f(l)) * kLn2 : -INFINITY;
   }
@@ -250,6 +255,14 @@ void launch_fwd_d(const AttnParams& p, hipStream_t s) {
   switch (p.D) {
     case 32: launch_fwd<T, 32>(p, s); break;
     case 64: launch_fwd<T, 64>(p, s); break;
+    case 80:
+      if constexpr (std::is_same<T, float>::value) {
+        fprintf(stderr, "fa_fwd: head dim 80 is 16-bit only\n");
+        abort();
+      } else {
+        launch_fwd<T, 80>(p, s);
+      }
+      break;
     case 128: launch_fwd<T, 128>(p, s); break;
     default: fprintf(stderr, "fa_fwd: unsupported head dim %d\n", p.D); abort();
   }

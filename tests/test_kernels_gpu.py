@@ -166,6 +166,17 @@ def test_flash_fwd_bwd(dt, D, causal, N):
     _check_flash(dt, D, causal, N, 2, 3)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("N", [128, 200, 512])
+def test_flash_fwd_bwd_d80_native(dt, causal, N):
+    """d_head 80 (the 2.7b model) runs natively (96-wide inside the kernel), no host padding."""
+    from cs336_systems.ops.flash_attention import _padded_d
+
+    assert _padded_d(80, dt) == 80
+    _check_flash(dt, 80, causal, N, 2, 3)
+
+
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("N", [200, 512])
@@ -278,7 +289,8 @@ def test_swiglu_fused_matches_reference():
 @pytest.mark.parametrize("heads", [4, 2])
 def test_fused_layout_matches_unfused(amp, heads):
     """Grouped QKV / W1|W3 GEMMs + AttentionCore + fp32-out dW == the unfused GPU path; heads=2 gives
-    d_head 80 (the 2.7b model's), where the grouped QKV GEMM feeds padded FA2 through strided views."""
+    d_head 80 (the 2.7b model's): native 80-wide FA2 in the fused core under bf16 autocast, the
+    host-padded FA2 through strided views in fp32."""
     from cs336_systems.models import BasicsTransformerLM
 
     torch.manual_seed(0)
