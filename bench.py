@@ -346,7 +346,7 @@ def main(argv=None):
     from cs336_systems.ops.gemm import _mode as gemm_mode
 
     gsel = {"blas": "hipblaslt default", "lt": "autotuned hipblaslt (cs336 lt_gemm)",
-            "best": "per-problem faster of hipblaslt default / autotuned lt_gemm", "hip": "cs336 MFMA GEMM"}[gemm_mode()]
+            "best": "per-problem fastest of hipblaslt default / autotuned lt_gemm / cs336 MFMA GEMM", "hip": "cs336 MFMA GEMM"}[gemm_mode()]
     out["config"]["gemm_selection"] = f"tunableop:{tmode}" if tmode else gsel if device.type == "cuda" else "torch cpu"
     if world > 1 or zero:
         out["dist"] = dist_diagnostics(ddp_model, comm_wait_ms, device, world)

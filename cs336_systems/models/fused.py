@@ -369,8 +369,10 @@ class FusedLinearFn(torch.autograd.Function):
         wt_shadow = compute_weight_t(list(weights)) if ctx.w_t else None
         if wt_shadow is not None:  # Wᵀ written by the fused AdamW together with the bf16 shadow
             w_saved = wt_shadow
-        elif ctx.w_t and torch.cuda.is_current_stream_capturing():
-            w_saved = _transpose(w)  # inside a HIP-graph capture: stay on the capturing stream
+        elif ctx.w_t and (torch.cuda.is_current_stream_capturing() or torch.compiler.is_compiling()):
+            # inside a HIP-graph capture or a torch.compile trace: stay on the current stream (no
+            # side-stream events in a captured/traced region)
+            w_saved = _transpose(w)
         elif ctx.w_t:
             main = torch.cuda.current_stream(x2.device)
             s = _side_stream(x2.device)

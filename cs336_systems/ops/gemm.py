@@ -13,11 +13,13 @@ default 48), fp32 output included, which TunableOp does not cover. On the XL sha
 is within noise of ``torch.mm``'s on most GEMMs and 1.1-1.5x faster on a few fp32-output weight
 gradients (``profiles/r1_lt_gemm_sweep*.json``), so ``blas`` stays the default.
 
-``CS336_GEMM=best`` takes the faster of the two per problem: the first time a (kind, shapes,
-strides, output) problem is seen outside graph capture, ``torch.mm`` and the autotuned ``lt_gemm``
-are each timed on it (HIP events on the current stream) and the winner is cached for the process.
-The sweep shows why neither alone is right: ``lt`` wins 1.2x on the QKV GEMMs and the lm_head weight
-gradient but loses 1.2x on the W1|W3 weight gradient from ``Xᵀ``.
+``CS336_GEMM=best`` takes the fastest per problem of hipBLASLt's default pick (``torch.mm``), the
+autotuned ``lt_gemm`` and the cs336 MFMA GEMM (where its tiling takes the shape): the first time a
+(kind, shapes, strides, output) problem is seen outside graph capture, each applicable candidate is
+timed on it (HIP events on the current stream) and the winner is cached for the process
+(``gemm_choices`` / ``gemm_timings``). The round-1 sweeps show why no single one is right: ``lt`` wins
+1.2x on the QKV GEMMs and the lm_head weight gradient but loses 1.2x on the W1|W3 weight gradient from
+``Xᵀ``; the cs336 GEMM wins the o-projection forward (967 vs 886 TFLOP/s).
 
 ``concurrent_safe=True`` (weight-gradient GEMMs issued on the dW side stream, i.e. possibly beside
 another GEMM) runs the cs336 MFMA GEMM: every workgroup owns whole output tiles and never waits for
@@ -65,28 +67,34 @@ def _time_ms(fn, reps: int = 5) -> float:
     return e0.elapsed_time(e1) / reps
 
 
-def _use_lt(kind: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None, lt_fn, blas_fn) -> bool:
-    """``lt`` mode: always; ``best`` mode: the cached per-problem winner (``torch.mm`` on ties and
+def _pick(kind: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None, cands: dict) -> str:
+    """``best`` mode: the fastest of ``cands`` (name -> zero-arg launcher) for this problem, timed
+    once with HIP events on the current stream and cached ("blas" on near-ties, within 3 %, and
     while a HIP graph is being captured, where nothing can be timed)."""
-    mode = _mode()
-    if mode == "lt":
-        return True
-    if mode != "best":
-        return False
     key = (kind, tuple(a.shape), a.stride(), tuple(b.shape), b.stride(),
            None if out is None else (out.dtype, out.stride()))
     hit = _BEST.get(key)
     if hit is None:
         if torch.cuda.is_current_stream_capturing():
-            return False
-        t_lt, t_blas = _time_ms(lt_fn), _time_ms(blas_fn)
-        hit = _BEST[key] = t_lt < 0.97 * t_blas
+            return "blas"
+        times = {name: _time_ms(fn) for name, fn in cands.items()}
+        best = min(times, key=times.get)
+        hit = _BEST[key] = best if times[best] < 0.97 * times["blas"] else "blas"
+        _BEST_TIMES[key] = times
     return hit
 
 
+_BEST_TIMES: dict = {}
+
+
 def gemm_choices() -> dict:
-    """``best`` mode decisions so far: problem key -> True when ``lt_gemm`` won."""
+    """``best`` mode decisions so far: problem key -> winning implementation ("blas", "lt" or
+    "cs336") and the measured ms of every candidate (``gemm_timings``)."""
     return dict(_BEST)
+
+
+def gemm_timings() -> dict:
+    return dict(_BEST_TIMES)
 
 
 def _lt_ok(*ts) -> bool:
@@ -97,26 +105,42 @@ def _ok(a, b, ta, tb) -> bool:
     return a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and ops().gemm_ok(a, b, ta, tb)
 
 
+def _select(kind, a, b, out, blas, lt, cs336) -> str:
+    """Implementation for this call: ``lt``/``hip`` modes force theirs where it applies, ``best``
+    times the applicable ones (``None`` = not applicable), ``blas`` is hipBLASLt's default."""
+    mode = _mode()
+    if mode == "lt" and lt is not None:
+        return "lt"
+    if mode == "hip" and cs336 is not None:
+        return "cs336"
+    if mode == "best":
+        cands = {"blas": blas}
+        if lt is not None:
+            cands["lt"] = lt
+        if cs336 is not None:
+            cands["cs336"] = cs336
+        return _pick(kind, a, b, out, cands) if len(cands) > 1 else "blas"
+    return "blas"
+
+
 def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``x @ w.T`` (forward of a linear layer)."""
-    if lt_gemm_enabled() and _lt_ok(x, w):
-        lt = lambda: ops().lt_gemm(x, w, False, True, torch.bfloat16)  # noqa: E731
-        if _use_lt("nt", x, w, None, lt, lambda: torch.mm(x, w.t())):
-            return lt()
-    if hip_gemm_enabled() and _ok(x, w, False, True):
-        return ops().gemm(x, w, False, True, torch.bfloat16, 0, 0, 0)
-    return torch.mm(x, w.t())
+    if _mode() == "blas":
+        return torch.mm(x, w.t())
+    blas = lambda: torch.mm(x, w.t())  # noqa: E731
+    lt = (lambda: ops().lt_gemm(x, w, False, True, torch.bfloat16)) if _lt_ok(x, w) else None
+    cs = (lambda: ops().gemm(x, w, False, True, torch.bfloat16, 0, 0, 0)) if _ok(x, w, False, True) else None
+    return {"blas": blas, "lt": lt, "cs336": cs}[_select("nt", x, w, None, blas, lt, cs)]()
 
 
 def mm_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``dy @ w`` (input gradient)."""
-    if lt_gemm_enabled() and _lt_ok(dy, w):
-        lt = lambda: ops().lt_gemm(dy, w, False, False, torch.bfloat16)  # noqa: E731
-        if _use_lt("nn", dy, w, None, lt, lambda: torch.mm(dy, w)):
-            return lt()
-    if hip_gemm_enabled() and _ok(dy, w, False, False):
-        return ops().gemm(dy, w, False, False, torch.bfloat16, 0, 0, 0)
-    return torch.mm(dy, w)
+    if _mode() == "blas":
+        return torch.mm(dy, w)
+    blas = lambda: torch.mm(dy, w)  # noqa: E731
+    lt = (lambda: ops().lt_gemm(dy, w, False, False, torch.bfloat16)) if _lt_ok(dy, w) else None
+    cs = (lambda: ops().gemm(dy, w, False, False, torch.bfloat16, 0, 0, 0)) if _ok(dy, w, False, False) else None
+    return {"blas": blas, "lt": lt, "cs336": cs}[_select("nn", dy, w, None, blas, lt, cs)]()
 
 
 NO_STREAM_K = 1  # lt_gemm flag: data-parallel hipBLASLt solutions only (none exist on gfx950 today)
@@ -141,23 +165,19 @@ def _dw_concurrent(dy, x, out):
 def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None = None,
                   concurrent_safe: bool = False) -> torch.Tensor:
     """``dy.T @ xt.T`` with an fp32 result: the weight gradient from a token-contiguous ``Xᵀ``
-    (K_in, tokens). hipBLASLt only: its NT kernels are the fast ones for this layout."""
+    (K_in, tokens). hipBLASLt only (default or autotuned): its NT kernels are the fast ones for
+    this layout and the cs336 GEMM has no (MN, K) orientation."""
     if concurrent_safe:
         raise RuntimeError("no concurrency-safe GEMM for the Xᵀ weight-gradient layout (dw_concurrent_ok)")
-    if lt_gemm_enabled() and _lt_ok(dy, xt) and (out is None or out.stride(1) == 1):
-        if out is None:
-            lt = lambda: ops().lt_gemm(dy, xt, True, True, torch.float32)  # noqa: E731
-            blas = lambda: torch.mm(dy.t(), xt.t(), out_dtype=torch.float32)  # noqa: E731
-        else:
-            lt = lambda: ops().lt_gemm_out(dy, xt, True, True, out)  # noqa: E731
-            blas = lambda: torch.mm(dy.t(), xt.t(), out_dtype=torch.float32, out=out)  # noqa: E731
-        if _use_lt("tt32", dy, xt, out, lt, blas):
-            r = lt()
-            return out if out is not None else r
-    if out is not None:
-        torch.mm(dy.t(), xt.t(), out_dtype=torch.float32, out=out)
-        return out
-    return torch.mm(dy.t(), xt.t(), out_dtype=torch.float32)
+    if out is None:
+        blas = lambda: torch.mm(dy.t(), xt.t(), out_dtype=torch.float32)  # noqa: E731
+        lt = lambda: ops().lt_gemm(dy, xt, True, True, torch.float32)  # noqa: E731
+    else:
+        blas = lambda: torch.mm(dy.t(), xt.t(), out_dtype=torch.float32, out=out)  # noqa: E731
+        lt = lambda: ops().lt_gemm_out(dy, xt, True, True, out)  # noqa: E731
+    use_lt = _mode() in ("lt", "best") and _lt_ok(dy, xt) and (out is None or out.stride(1) == 1)
+    r = (lt if use_lt and _select("tt32", dy, xt, out, blas, lt, None) == "lt" else blas)()
+    return out if out is not None else r
 
 
 def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
@@ -165,25 +185,23 @@ def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = Non
     """``dy.T @ x`` with an fp32 result (weight gradient), written into ``out`` when given."""
     if concurrent_safe:
         return _dw_concurrent(dy, x, out)
-    if lt_gemm_enabled() and _lt_ok(dy, x) and (out is None or out.stride(1) == 1):
-        if out is None:
-            lt = lambda: ops().lt_gemm(dy, x, True, False, torch.float32)  # noqa: E731
-            blas = lambda: torch.mm(dy.t(), x, out_dtype=torch.float32)  # noqa: E731
-        else:
-            lt = lambda: ops().lt_gemm_out(dy, x, True, False, out)  # noqa: E731
-            blas = lambda: torch.mm(dy.t(), x, out_dtype=torch.float32, out=out)  # noqa: E731
-        if _use_lt("tn32", dy, x, out, lt, blas):
-            r = lt()
-            return out if out is not None else r
-    if hip_gemm_enabled() and _ok(dy, x, True, False):
-        if out is not None:
-            ops().gemm_out(dy, x, True, False, out, False, 0, 0, 0)
-            return out
-        return ops().gemm(dy, x, True, False, torch.float32, 0, 0, 0)
-    if out is not None:
-        torch.mm(dy.t(), x, out_dtype=torch.float32, out=out)
-        return out
-    try:
-        return torch.mm(dy.t(), x, out_dtype=torch.float32)
-    except (TypeError, RuntimeError):
-        return torch.mm(dy.t(), x).float()
+    if out is None:
+        def blas():
+            try:
+                return torch.mm(dy.t(), x, out_dtype=torch.float32)
+            except (TypeError, RuntimeError):
+                return torch.mm(dy.t(), x).float()
+    else:
+        blas = lambda: torch.mm(dy.t(), x, out_dtype=torch.float32, out=out)  # noqa: E731
+    if _mode() == "blas" or not dy.is_cuda:
+        r = blas()
+        return out if out is not None else r
+    lt_ok = _lt_ok(dy, x) and (out is None or out.stride(1) == 1)
+    if out is None:
+        lt = (lambda: ops().lt_gemm(dy, x, True, False, torch.float32)) if lt_ok else None
+        cs = (lambda: ops().gemm(dy, x, True, False, torch.float32, 0, 0, 0)) if _ok(dy, x, True, False) else None
+    else:
+        lt = (lambda: ops().lt_gemm_out(dy, x, True, False, out)) if lt_ok else None
+        cs = (lambda: ops().gemm_out(dy, x, True, False, out, False, 0, 0, 0)) if _ok(dy, x, True, False) else None
+    r = {"blas": blas, "lt": lt, "cs336": cs}[_select("tn32", dy, x, out, blas, lt, cs)]()
+    return out if out is not None else r

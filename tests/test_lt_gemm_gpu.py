@@ -131,3 +131,30 @@ def test_best_mode_picks_per_problem_and_matches_fp32(monkeypatch):
     n = len(choices)
     gemm.mm_nt(x, w)
     assert len(gemm.gemm_choices()) == n  # cached, not re-timed
+
+
+def test_best_mode_times_cs336_gemm_where_it_applies(monkeypatch):
+    """At shapes the cs336 MFMA GEMM tiles (160/256 multiples, K % 64 == 0) `best` times it next to
+    hipBLASLt's default and the autotuned lt_gemm, and any winner is numerically right."""
+    from cs336_systems.ops import gemm
+
+    monkeypatch.setenv("CS336_GEMM", "best")
+    gemm._BEST.clear()
+    gemm._BEST_TIMES.clear()
+    torch.manual_seed(4)
+    T, K, N = 2560, 1600, 1600  # XL o-projection widths at 2560 tokens
+    x = torch.randn(T, K, device=DEV).bfloat16()
+    w = torch.randn(N, K, device=DEV).bfloat16()
+    dy = torch.randn(T, N, device=DEV).bfloat16()
+    y = gemm.mm_nt(x, w)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), rtol=1e-2, atol=1e-2 * K**0.5 * 4)
+    dx = gemm.mm_nn(dy, w)
+    torch.testing.assert_close(dx.float(), dy.float() @ w.float(), rtol=1e-2, atol=1e-2 * N**0.5 * 4)
+    ref_dw = dy.float().t() @ x.float()
+    dw = gemm.mm_tn_fp32(dy, x)
+    torch.testing.assert_close(dw, ref_dw, rtol=1e-3, atol=1e-3 * ref_dw.abs().max().item())
+    timed = gemm.gemm_timings()
+    assert len(timed) == 3
+    for key, times in timed.items():
+        assert set(times) == {"blas", "lt", "cs336"}, (key, times)
+        assert gemm.gemm_choices()[key] in times
