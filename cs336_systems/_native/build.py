@@ -143,10 +143,25 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        _check_loadable(tmp)
         os.replace(tmp, LIB)
         if verbose:
             print(f"linked {LIB}", flush=True)
     return LIB
+
+
+def _check_loadable(path: str) -> None:
+    """dlopen the freshly linked library (RTLD_NOW): an unresolved symbol -- e.g. a kernel whose host
+    stub the compiler referenced but never emitted -- fails the build here instead of on the GPU box."""
+    import ctypes
+
+    import torch  # noqa: F401  (loads libc10/libtorch the extension links against)
+
+    try:
+        ctypes.CDLL(path, mode=os.RTLD_NOW | os.RTLD_LOCAL)
+    except OSError as e:
+        os.remove(path)
+        raise RuntimeError(f"built library does not load: {e}") from e
 
 
 def main(argv=None):

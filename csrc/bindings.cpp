@@ -83,6 +83,11 @@ void fill_attn(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, c
   // heads whose K+V fit one XCD's 4 MB L2 form one level-major group (tile_order, fa_common.h)
   const int64_t kv_head = 2 * (int64_t)p.Nk * p.D * (int64_t)q.element_size();
   p.lpt_group = (int)std::max<int64_t>(1, std::min<int64_t>(1 << 20, (int64_t(4) << 20) / std::max<int64_t>(kv_head, 1)));
+  static const int dma = [] {
+    const char* e = std::getenv("CS336_FA_DMA");
+    return e ? std::atoi(e) : 1;
+  }();
+  p.dma = dma;
 }
 
 using OptT = std::optional<at::Tensor>;

@@ -24,7 +24,7 @@ namespace fa {
 // ============================================================================================
 // dQ (+ delta) kernel
 // ============================================================================================
-template <typename T, int D, bool CAUSAL, bool ROPE>
+template <typename T, int D, bool CAUSAL, bool ROPE, bool DMA>
 __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
   const AttnParams p = bp.f;  // by value: a reference would spill the kernarg struct to scratch
@@ -41,8 +41,10 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   static_assert(BN * CPR % 256 == 0, "staging rounds must be whole");
   constexpr int NDT = DP / 32;
   constexpr bool PREFETCH = !(F32 && D == 128);
+  static_assert(!DMA || (!F32 && !ROPE), "LDS-DMA staging: 16-bit, no RoPE-on-load");
+  constexpr int NS = DMA ? 3 : 2;  // K/V ring depth
 
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+  __shared__ __attribute__((aligned(1024))) char smem[NS * 2 * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int l32 = lane & 31, hh = lane >> 5;
@@ -129,19 +131,11 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   for (int i = 0; i < NDT; ++i) dq[i] = zero16();
   const float c2 = p.scale * kLog2e;
 
-  if (ntiles > 0) {
-    gload(0);
-    swrite(0);
-  }
-  __syncthreads();
-
-  for (int j = 0; j < ntiles; ++j) {
-    const int buf = PREFETCH ? (j & 1) : 0;
-    if (PREFETCH && j + 1 < ntiles) gload(j + 1);
+  // one K/V tile: S^T, dP^T, dS^T, dQ^T += K^T dS^T (Ks: the tile's K image, V after it)
+  auto tile = [&](int j, const char* Ks) {
     const int kt0 = j * BN;
     const bool active = !CAUSAL || kt0 <= qw0 + 31;
     if (active) {
-      const char* Ks = smem + buf * 2 * TILE;
       const char* Vs = Ks + TILE;
       f32x16 s[NT], dp[NT];
 #pragma unroll
@@ -208,16 +202,54 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
               dq[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Ks, 32 * t, s2, dt, lane), pf[t][s2], dq[dt]);
       }
     }
-    if (j + 1 < ntiles) {
-      if (PREFETCH) {
-        swrite(buf ^ 1);
-      } else {
-        __syncthreads();
-        gload(j + 1);
-        swrite(0);
-      }
+  };
+
+  if constexpr (DMA) {
+    using Dma = TileDma<BN, RB, CREAL, ES>;
+    Dma kd, vd;
+    kd.init(wave, lane, p.k_sn);
+    vd.init(wave, lane, p.v_sn);
+    if (D != DP || p.Nk % BN != 0) {  // some slots are read out of range: start from zeros
+      lds_zero(smem, NS * 2 * TILE);
+      __syncthreads();
+    }
+    auto issue = [&](int j) {
+      char* Ks = smem + (j % NS) * 2 * TILE;
+      const int rows = min(BN, p.Nk - j * BN);
+      kd.issue(Kp + (int64_t)j * BN * p.k_sn, rows, p.k_sn, Ks, wave);
+      vd.issue(Vp + (int64_t)j * BN * p.v_sn, rows, p.v_sn, Ks + TILE, wave);
+    };
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t)
+      if (t < ntiles) issue(t);
+    for (int j = 0; j < ntiles; ++j) {
+      if (NS == 3 && j + 1 < ntiles) wait_vmcnt<2 * Dma::PER_WAVE>();
+      else wait_vmcnt<0>();
+      __syncthreads();
+      if (j + NS - 1 < ntiles) issue(j + NS - 1);
+      tile(j, smem + (j % NS) * 2 * TILE);
+    }
+  } else {
+    if (ntiles > 0) {
+      gload(0);
+      swrite(0);
     }
     __syncthreads();
+    for (int j = 0; j < ntiles; ++j) {
+      const int buf = PREFETCH ? (j & 1) : 0;
+      if (PREFETCH && j + 1 < ntiles) gload(j + 1);
+      tile(j, smem + buf * 2 * TILE);
+      if (j + 1 < ntiles) {
+        if (PREFETCH) {
+          swrite(buf ^ 1);
+        } else {
+          __syncthreads();
+          gload(j + 1);
+          swrite(0);
+        }
+      }
+      __syncthreads();
+    }
   }
 
   if (valid_q) {
@@ -243,8 +275,13 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
 // Occupancy hint: 16-bit D=64 asks for two workgroups per CU explicitly (same occupancy as without
 // the hint, but the register schedule it produces measured 2-5 % faster at N=512 and 4096); at D=128
 // the hint spills the resident K/V fragments (1153 -> 1461 us at N=4096), so D=128 runs one per CU.
-template <typename T, int D, bool CAUSAL, bool ROPE>
-__global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 2 : 1) void fa_bwd_dkdv_kernel(const AttnBwdParams bp) {
+template <typename T, int D>
+constexpr int dkdv_min_waves() {
+  return (D == 64 && !std::is_same<T, float>::value) ? 2 : 1;
+}
+
+template <typename T, int D, bool CAUSAL, bool ROPE, bool DMA>
+__global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
   const AttnParams p = bp.f;  // by value: a reference would spill the kernarg struct to scratch
   constexpr bool F32 = std::is_same<T, float>::value;
@@ -261,8 +298,13 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
   static_assert(BQ * CPR % 256 == 0, "staging rounds must be whole");
   constexpr int NDT = DP / 32;
   constexpr bool PREFETCH = !(F32 && D == 128);
+  static_assert(!DMA || (!F32 && !ROPE), "LDS-DMA staging: 16-bit, no RoPE-on-load");
+  // LDS-DMA slot: Q, dO images, then L and delta in 1 KB regions (one wave-instruction each)
+  constexpr int BUFD = 2 * TILE + 2048;
+  constexpr int NS = DMA ? (DP <= 96 ? 3 : 2) : (PREFETCH ? 2 : 1);
+  constexpr int SLOT = DMA ? BUFD : BUF;
 
-  __shared__ __attribute__((aligned(16))) char smem[(PREFETCH ? 2 : 1) * BUF];
+  __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int l32 = lane & 31, hh = lane >> 5;
@@ -353,22 +395,16 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
   }
   const float c2 = p.scale * kLog2e;
 
-  if (qt_begin < qt_end) {
-    gload(qt_begin);
-    swrite(0);
-  }
-  __syncthreads();
-
-  for (int it = qt_begin; it < qt_end; ++it) {
-    const int buf = PREFETCH ? ((it - qt_begin) & 1) : 0;
-    if (PREFETCH && it + 1 < qt_end) gload(it + 1);
+  // one query tile: S, dP, P, dS, dV^T += dO^T P, dK^T += Q^T dS (Qs: the slot's Q image, dO after it)
+  auto tile = [&](int it, const char* Qs) {
     const int qt0 = it * BQ;
     const bool active = !CAUSAL || (qt0 + BQ - 1 >= kw0);
     if (active) {
-      const char* Qs = smem + buf * BUF;
       const char* dOs = Qs + TILE;
+      // L and delta rows: pre-scaled L2 after the VGPR staging, raw natural-log L after LDS-DMA
       const float* Ls = reinterpret_cast<const float*>(Qs + 2 * TILE);
-      const float* Ds = Ls + BQ;
+      const float* Ds = DMA ? Ls + 256 : Ls + BQ;
+      const float lscale = DMA ? kLog2e : 1.f;
       f32x16 s[NT], dp[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -399,7 +435,7 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
         }
       }
       // P = exp2(S*c - L2[q]); dS = P (dP - delta[q]); rows (q) are in registers
-      const bool need_mask = CAUSAL && (qt0 < kw0 + 31);
+      const bool need_mask = (CAUSAL && (qt0 < kw0 + 31)) || (DMA && qt0 + BQ > p.Nq);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -412,8 +448,8 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int r = 4 * g + u;
-            float pv = fexp2(fmaf(s[t][r], c2, -Lv[u]));
-            if (need_mask && (krow > qt0 + qr + u)) pv = 0.f;
+            float pv = fexp2(fmaf(s[t][r], c2, -Lv[u] * lscale));
+            if (need_mask && ((CAUSAL && krow > qt0 + qr + u) || (DMA && qt0 + qr + u >= p.Nq))) pv = 0.f;
             s[t][r] = pv;
             dp[t][r] = pv * (dp[t][r] - Dv[u]);
           }
@@ -449,16 +485,61 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
             }
       }
     }
-    if (it + 1 < qt_end) {
-      if (PREFETCH) {
-        swrite(buf ^ 1);
-      } else {
-        __syncthreads();
-        gload(it + 1);
-        swrite(0);
-      }
+  };
+
+  if constexpr (DMA) {
+    using Dma = TileDma<BQ, RB, CREAL, ES>;
+    Dma qd, dd;
+    qd.init(wave, lane, p.q_sn);
+    dd.init(wave, lane, bp.do_sn);
+    const uint32_t row_off = lane < 16 ? 16u * lane : 0x80000000u;  // L / delta: 64 floats = 16 lanes
+    if (D != DP || p.Nq % BQ != 0) {  // some slots are read out of range: start from zeros
+      lds_zero(smem, NS * SLOT);
+      __syncthreads();
+    }
+    auto issue = [&](int it) {
+      char* base = smem + ((it - qt_begin) % NS) * SLOT;
+      const int rows = min(BQ, p.Nq - it * BQ);
+      qd.issue(Qp + (int64_t)it * BQ * p.q_sn, rows, p.q_sn, base, wave);
+      dd.issue(dOp + (int64_t)it * BQ * bp.do_sn, rows, bp.do_sn, base + TILE, wave);
+      // every wave loads the same L / delta rows (identical bytes): uniform vmcnt accounting
+      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)(Lp + it * BQ), (short)0, rows * 4, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(Dp + it * BQ), (short)0, rows * 4, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (__attribute__((address_space(3))) void*)(base + 2 * TILE), 16, row_off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (__attribute__((address_space(3))) void*)(base + 2 * TILE + 1024), 16, row_off, 0, 0, 0);
+    };
+    constexpr int PER_TILE = 2 * Dma::PER_WAVE + 2;
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t)
+      if (qt_begin + t < qt_end) issue(qt_begin + t);
+    for (int it = qt_begin; it < qt_end; ++it) {
+      if (NS == 3 && it + 1 < qt_end) wait_vmcnt<PER_TILE>();
+      else wait_vmcnt<0>();
+      __syncthreads();
+      if (it + NS - 1 < qt_end) issue(it + NS - 1);
+      tile(it, smem + ((it - qt_begin) % NS) * SLOT);
+    }
+  } else {
+    if (qt_begin < qt_end) {
+      gload(qt_begin);
+      swrite(0);
     }
     __syncthreads();
+    for (int it = qt_begin; it < qt_end; ++it) {
+      const int buf = PREFETCH ? ((it - qt_begin) & 1) : 0;
+      if (PREFETCH && it + 1 < qt_end) gload(it + 1);
+      tile(it, smem + buf * BUF);
+      if (it + 1 < qt_end) {
+        if (PREFETCH) {
+          swrite(buf ^ 1);
+        } else {
+          __syncthreads();
+          gload(it + 1);
+          swrite(0);
+        }
+      }
+      __syncthreads();
+    }
   }
 
   if (valid_k) {
@@ -480,22 +561,49 @@ __global__ __launch_bounds__(256, (D == 64 && !std::is_same<T, float>::value) ? 
   }
 }
 
+// Explicit instantiation of the LDS-DMA variants (hipcc referenced some implicit ones from the launch
+// chain without emitting their host stubs; see fa_fwd.hip)
+#define CS336_FA_BWD_DMA(T, D)                                                                  \
+  template __global__ void fa_bwd_dq_kernel<T, D, false, false, true>(const AttnBwdParams);   \
+  template __global__ void fa_bwd_dq_kernel<T, D, true, false, true>(const AttnBwdParams);    \
+  template __global__ void fa_bwd_dkdv_kernel<T, D, false, false, true>(const AttnBwdParams); \
+  template __global__ void fa_bwd_dkdv_kernel<T, D, true, false, true>(const AttnBwdParams);
+CS336_FA_BWD_DMA(BF16, 32)
+CS336_FA_BWD_DMA(BF16, 64)
+CS336_FA_BWD_DMA(BF16, 80)
+CS336_FA_BWD_DMA(BF16, 128)
+CS336_FA_BWD_DMA(F16, 32)
+CS336_FA_BWD_DMA(F16, 64)
+CS336_FA_BWD_DMA(F16, 80)
+CS336_FA_BWD_DMA(F16, 128)
+#undef CS336_FA_BWD_DMA
+
+template <typename T, int D, bool C, bool R, bool DMA>
+void launch_bwd_v(const AttnBwdParams& bp, hipStream_t s, dim3 gq, dim3 gk, dim3 block) {
+  hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, C, R, DMA>), gq, block, 0, s, bp);
+  hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, C, R, DMA>), gk, block, 0, s, bp);
+}
+
+template <typename T, int D, bool C>
+void launch_bwd_c(const AttnBwdParams& bp, hipStream_t s, dim3 gq, dim3 gk, dim3 block) {
+  if (bp.f.rope_cos != nullptr) {
+    launch_bwd_v<T, D, C, true, false>(bp, s, gq, gk, block);
+  } else if constexpr (!std::is_same<T, float>::value) {
+    if (bp.f.dma) launch_bwd_v<T, D, C, false, true>(bp, s, gq, gk, block);
+    else launch_bwd_v<T, D, C, false, false>(bp, s, gq, gk, block);
+  } else {
+    launch_bwd_v<T, D, C, false, false>(bp, s, gq, gk, block);
+  }
+}
+
 template <typename T, int D>
 void launch_bwd(const AttnBwdParams& bp, hipStream_t s) {
   const AttnParams& p = bp.f;
   const int nqb = (p.Nq + 127) / 128;
   const int nkb = (p.Nk + 127) / 128;
   const dim3 gq((unsigned)(nqb * p.B * p.H)), gk((unsigned)(nkb * p.B * p.H)), block(256);
-  auto go = [&](auto causal, auto rope) {
-    constexpr bool C = decltype(causal)::value, R = decltype(rope)::value;
-    hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, C, R>), gq, block, 0, s, bp);
-    hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, C, R>), gk, block, 0, s, bp);
-  };
-  const bool rope = p.rope_cos != nullptr;
-  if (p.causal && rope) go(std::true_type{}, std::true_type{});
-  else if (p.causal) go(std::true_type{}, std::false_type{});
-  else if (rope) go(std::false_type{}, std::true_type{});
-  else go(std::false_type{}, std::false_type{});
+  if (p.causal) launch_bwd_c<T, D, true>(bp, s, gq, gk, block);
+  else launch_bwd_c<T, D, false>(bp, s, gq, gk, block);
 }
 
 template <typename T>

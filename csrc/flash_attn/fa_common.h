@@ -260,6 +260,50 @@ __device__ __forceinline__ void rope_inv4(float& v0, float& v1, float& v2, float
   v0 = a0; v1 = a1; v2 = b0; v3 = b1;
 }
 
+// ---- direct-to-LDS tile staging (buffer_load ... lds) ------------------------------------------
+// One ROWS x RB tile of a strided [row][d] operand (K, V, Q or dO of one head) goes global -> LDS
+// without VGPRs: each wave-instruction moves 64 lanes x 16 B into 1 KB of consecutive LDS, so the
+// image's XOR swizzle is applied to each lane's GLOBAL source chunk (slot q = row r, physical chunk
+// pc holds logical chunk pc ^ swz(r)) and undone by the usual lds_off reads. Rows past the tile's
+// valid count and the zero padding chunks of d_head 80 (chunk >= CREAL) read out of the buffer
+// descriptor's range; the kernel zero-fills its LDS ring once at entry, so such slots hold zeros or
+// finite stale rows, which the masks turn into exact zeros (P = 0 for keys >= Nk / queries >= Nq).
+template <int ROWS, int RB, int CREAL, int ES>
+struct TileDma {
+  static constexpr int CPR = RB / 16;
+  static constexpr int PER_WAVE = ROWS * CPR / 256;  // 4 waves x 64 lanes per round
+  static_assert(ROWS * CPR % 256 == 0, "DMA rounds must be whole");
+  uint32_t voff[PER_WAVE];  // per-lane byte offsets from the tile's first row (0x80000000: padding)
+
+  __device__ __forceinline__ void init(int wave, int lane, int64_t ld) {
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int q = (i * 4 + wave) * 64 + lane;
+      const int r = q / CPR, pc = q % CPR, c = pc ^ swz<RB>(r);
+      voff[i] = c < CREAL ? (uint32_t)(((int64_t)r * ld + c * (16 / ES)) * ES) : 0x80000000u;
+    }
+  }
+  // rows_valid rows from `tile` are loaded; (wave-uniform arguments)
+  __device__ __forceinline__ void issue(const void* tile, int rows_valid, int64_t ld, char* img, int wave) const {
+    const uint32_t bytes = rows_valid > 0 ? (uint32_t)((int64_t)(rows_valid - 1) * ld * ES + CREAL * 16) : 0u;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)tile, (short)0, (int)bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(img + 1024 * (i * 4 + wave)),
+                                               16, voff[i], 0, 0, 0);
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// zero a block of LDS (all 256 threads; bytes % 4096 == 0)
+__device__ __forceinline__ void lds_zero(char* p, int bytes) {
+  for (int o = threadIdx.x * 16; o < bytes; o += 256 * 16) *reinterpret_cast<uint4*>(p + o) = make_uint4(0, 0, 0, 0);
+}
+
 // key (or row) index held by accumulator register `reg` of lane-half h in a 32x32 tile
 __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 

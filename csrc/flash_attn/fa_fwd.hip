@@ -19,8 +19,15 @@
 namespace cs336 {
 namespace fa {
 
-template <typename T, int D, bool CAUSAL, bool ROPE>
-__global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
+// 16-bit variants ask for two workgroups per CU (<= 256 VGPRs): without the hint the LDS-DMA variant
+// at d 128 took 260 registers, ran one workgroup per CU and lost 37 % (causal, N 4096)
+template <typename T>
+constexpr int fwd_min_waves() {
+  return std::is_same<T, float>::value ? 1 : 2;
+}
+
+template <typename T, int D, bool CAUSAL, bool ROPE, bool DMA>
+__global__ __launch_bounds__(256, fwd_min_waves<T>()) void fa_fwd_kernel(const AttnParams p) {
   typedef typename Elem<T>::storage S;
   constexpr bool F32 = std::is_same<T, float>::value;
   constexpr int ES = sizeof(S);
@@ -35,8 +42,11 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
   static_assert(BN * CPR % 256 == 0, "staging rounds must be whole");
   constexpr int NDT = DP / 32;         // 32-wide d tiles of O^T
   constexpr bool PREFETCH = !(F32 && D == 128);
+  static_assert(!DMA || (!F32 && !ROPE), "LDS-DMA staging: 16-bit, no RoPE-on-load");
+  // LDS-DMA ring depth: 3 K/V stages (two tiles in flight) up to 96-wide rows, 2 at d 128
+  constexpr int NS = DMA ? (DP <= 96 ? 3 : 2) : 2;
 
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+  __shared__ __attribute__((aligned(1024))) char smem[NS * 2 * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int l32 = lane & 31, hh = lane >> 5;
@@ -110,19 +120,11 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
   for (int i = 0; i < NDT; ++i) o[i] = zero16();
   const float c2 = p.scale * kLog2e;
 
-  if (ntiles > 0) {
-    gload(0);
-    swrite(0);
-  }
-  __syncthreads();
-
-  for (int j = 0; j < ntiles; ++j) {
-    const int buf = PREFETCH ? (j & 1) : 0;
-    if (PREFETCH && j + 1 < ntiles) gload(j + 1);
+  // one K/V tile's work: S^T, mask, online softmax, O^T += V^T P^T (Ks: the tile's K image, V after it)
+  auto tile = [&](int j, const char* Ks) {
     const int kt0 = j * BN;
     const bool active = !CAUSAL || kt0 <= qw0 + 31;
     if (active) {
-      const char* Ks = smem + buf * 2 * TILE;
       const char* Vs = Ks + TILE;
       f32x16 s[2];
       // ---- S^T = K Q^T ----
@@ -209,16 +211,56 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
               o[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Vs, 32 * t, s2, dt, lane), pf[t][s2], o[dt]);
       }
     }
-    if (j + 1 < ntiles) {
-      if (PREFETCH) {
-        swrite(buf ^ 1);
-      } else {
-        __syncthreads();
-        gload(j + 1);
-        swrite(0);
-      }
+  };
+
+  if constexpr (DMA) {
+    using Dma = TileDma<BN, RB, CREAL, ES>;
+    Dma kd, vd;
+    kd.init(wave, lane, p.k_sn);
+    vd.init(wave, lane, p.v_sn);
+    if (D != DP || p.Nk % BN != 0) {  // some slots are read out of range: start from zeros
+      lds_zero(smem, NS * 2 * TILE);
+      __syncthreads();
+    }
+    auto issue = [&](int j) {
+      char* Ks = smem + (j % NS) * 2 * TILE;
+      const int rows = min(BN, p.Nk - j * BN);
+      kd.issue(Kp + (int64_t)j * BN * p.k_sn, rows, p.k_sn, Ks, wave);
+      vd.issue(Vp + (int64_t)j * BN * p.v_sn, rows, p.v_sn, Ks + TILE, wave);
+    };
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t)
+      if (t < ntiles) issue(t);
+    for (int j = 0; j < ntiles; ++j) {
+      // this wave's pieces of tile j have landed once only the younger tiles' DMAs are in flight;
+      // the barrier then publishes every wave's pieces and retires all reads of tile j-1's slot
+      if (NS == 3 && j + 1 < ntiles) wait_vmcnt<2 * Dma::PER_WAVE>();
+      else wait_vmcnt<0>();
+      __syncthreads();
+      if (j + NS - 1 < ntiles) issue(j + NS - 1);
+      tile(j, smem + (j % NS) * 2 * TILE);
+    }
+  } else {
+    if (ntiles > 0) {
+      gload(0);
+      swrite(0);
     }
     __syncthreads();
+    for (int j = 0; j < ntiles; ++j) {
+      const int buf = PREFETCH ? (j & 1) : 0;
+      if (PREFETCH && j + 1 < ntiles) gload(j + 1);
+      tile(j, smem + buf * 2 * TILE);
+      if (j + 1 < ntiles) {
+        if (PREFETCH) {
+          swrite(buf ^ 1);
+        } else {
+          __syncthreads();
+          gload(j + 1);
+          swrite(0);
+        }
+      }
+      __syncthreads();
+    }
   }
 
   // ---- epilogue ----
@@ -239,15 +281,39 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const AttnParams p) {
   }
 }
 
+// Explicit instantiation of the LDS-DMA variants: hipcc (ROCm 7.2) referenced some of them from the
+// launch chain below without emitting their host stubs (undefined __device_stub__ at load time).
+#define CS336_FA_FWD_DMA(T, D)                                                     \
+  template __global__ void fa_fwd_kernel<T, D, false, false, true>(const AttnParams); \
+  template __global__ void fa_fwd_kernel<T, D, true, false, true>(const AttnParams);
+CS336_FA_FWD_DMA(BF16, 32)
+CS336_FA_FWD_DMA(BF16, 64)
+CS336_FA_FWD_DMA(BF16, 80)
+CS336_FA_FWD_DMA(BF16, 128)
+CS336_FA_FWD_DMA(F16, 32)
+CS336_FA_FWD_DMA(F16, 64)
+CS336_FA_FWD_DMA(F16, 80)
+CS336_FA_FWD_DMA(F16, 128)
+#undef CS336_FA_FWD_DMA
+
+template <typename T, int D, bool C>
+void launch_fwd_c(const AttnParams& p, hipStream_t s, dim3 grid, dim3 block) {
+  if (p.rope_cos != nullptr) {
+    hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, true, false>), grid, block, 0, s, p);
+  } else if constexpr (!std::is_same<T, float>::value) {
+    if (p.dma) hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, true>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, false>), grid, block, 0, s, p);
+  } else {
+    hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, false>), grid, block, 0, s, p);
+  }
+}
+
 template <typename T, int D>
 void launch_fwd(const AttnParams& p, hipStream_t s) {
   const int nqb = (p.Nq + 127) / 128;
   const dim3 grid((unsigned)(nqb * p.B * p.H)), block(256);
-  const bool rope = p.rope_cos != nullptr;
-  if (p.causal && rope) hipLaunchKernelGGL((fa_fwd_kernel<T, D, true, true>), grid, block, 0, s, p);
-  else if (p.causal) hipLaunchKernelGGL((fa_fwd_kernel<T, D, true, false>), grid, block, 0, s, p);
-  else if (rope) hipLaunchKernelGGL((fa_fwd_kernel<T, D, false, true>), grid, block, 0, s, p);
-  else hipLaunchKernelGGL((fa_fwd_kernel<T, D, false, false>), grid, block, 0, s, p);
+  if (p.causal) launch_fwd_c<T, D, true>(p, s, grid, block);
+  else launch_fwd_c<T, D, false>(p, s, grid, block);
 }
 
 template <typename T>
