@@ -83,11 +83,16 @@ void fill_attn(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, c
   // heads whose K+V fit one XCD's 4 MB L2 form one level-major group (tile_order, fa_common.h)
   const int64_t kv_head = 2 * (int64_t)p.Nk * p.D * (int64_t)q.element_size();
   p.lpt_group = (int)std::max<int64_t>(1, std::min<int64_t>(1 << 20, (int64_t(4) << 20) / std::max<int64_t>(kv_head, 1)));
-  static const int dma = [] {
+  // LDS-DMA staging (fa_common.h TileDma), measured per kernel at N 4096 (scripts/fa_ab.py):
+  // forward +12-24 % without the causal mask and +3 % at d 128 causal, -2 % at d 64 causal; the
+  // backward kernels lose 2-7 % (their time is not in the tile loads). CS336_FA_DMA: unset = that
+  // choice, 0 = never, 1 = every forward, 2 = forward and backward.
+  static const int dma_env = [] {
     const char* e = std::getenv("CS336_FA_DMA");
-    return e ? std::atoi(e) : 1;
+    return e && *e ? std::atoi(e) : -1;
   }();
-  p.dma = dma;
+  if (dma_env < 0) p.dma = (!causal || p.D >= 128) ? 1 : 0;
+  else p.dma = dma_env == 0 ? 0 : (dma_env == 1 ? 1 : 3);
 }
 
 using OptT = std::optional<at::Tensor>;

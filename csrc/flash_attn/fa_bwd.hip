@@ -589,7 +589,7 @@ void launch_bwd_c(const AttnBwdParams& bp, hipStream_t s, dim3 gq, dim3 gk, dim3
   if (bp.f.rope_cos != nullptr) {
     launch_bwd_v<T, D, C, true, false>(bp, s, gq, gk, block);
   } else if constexpr (!std::is_same<T, float>::value) {
-    if (bp.f.dma) launch_bwd_v<T, D, C, false, true>(bp, s, gq, gk, block);
+    if (bp.f.dma & 2) launch_bwd_v<T, D, C, false, true>(bp, s, gq, gk, block);
     else launch_bwd_v<T, D, C, false, false>(bp, s, gq, gk, block);
   } else {
     launch_bwd_v<T, D, C, false, false>(bp, s, gq, gk, block);

@@ -301,7 +301,7 @@ void launch_fwd_c(const AttnParams& p, hipStream_t s, dim3 grid, dim3 block) {
   if (p.rope_cos != nullptr) {
     hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, true, false>), grid, block, 0, s, p);
   } else if constexpr (!std::is_same<T, float>::value) {
-    if (p.dma) hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, true>), grid, block, 0, s, p);
+    if (p.dma & 1) hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, true>), grid, block, 0, s, p);
     else hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, false>), grid, block, 0, s, p);
   } else {
     hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, false>), grid, block, 0, s, p);

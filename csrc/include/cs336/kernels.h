@@ -126,8 +126,8 @@ struct AttnParams {
   // level first within each XCD's heads (longest-processing-time order, see tile_order in fa_common.h)
   int order = 1;
   int lpt_group = 1 << 20;  // heads per level-major group (sized by the host to the L2, fill_attn)
-  // tile staging: 1 = K/V (fwd, dQ) and Q/dO (dK/dV) go global -> LDS by buffer_load ... lds (16-bit,
-  // no RoPE-on-load), 0 = through VGPRs (CS336_FA_DMA, fill_attn)
+  // tile staging by buffer_load ... lds (16-bit, no RoPE-on-load) instead of through VGPRs: bit 0 the
+  // forward's K/V tiles, bit 1 the backward's K/V (dQ) and Q/dO (dK/dV) tiles (CS336_FA_DMA, fill_attn)
   int dma = 1;
 };
 
