@@ -324,6 +324,11 @@ def _transpose_weight() -> bool:
     return os.environ.get("CS336_WT", "1") != "0"
 
 
+def attn_out_transposed() -> bool:
+    """The FA2 forward also writes Oᵀ for the output projection's weight gradient (CS336_OT=0: off)."""
+    return os.environ.get("CS336_OT", "1") != "0"
+
+
 def _mark_side_work() -> None:
     _state["dirty"] = True
     if not _state["callback"]:
@@ -349,7 +354,7 @@ class FusedLinearFn(torch.autograd.Function):
     views of one fp32 dW."""
 
     @staticmethod
-    def forward(ctx, x, *weights):
+    def forward(ctx, x, xt_given, *weights):
         amp = torch.is_autocast_enabled("cuda") and x.is_cuda
         cdt = torch.get_autocast_dtype("cuda") if amp else weights[0].dtype
         w = compute_weight(list(weights), cdt)
@@ -359,8 +364,17 @@ class FusedLinearFn(torch.autograd.Function):
         y = gemm.mm_nt(x2, w)
         # For wide projections (N_out >= r * K_in, e.g. W1|W3: 12800 vs 1600) save Xᵀ instead of X:
         # the weight-gradient GEMM dYᵀX then reads both operands token-contiguous, which hipBLASLt
-        # runs 1.4x faster on MI355X (profiles/r1_gemm_dw_layouts.json), for one small transpose
-        ctx.xt = x2.is_cuda and any(ctx.needs_input_grad[1:]) and _save_transposed(x2.shape[1], w.shape[0])
+        # runs 1.4x faster on MI355X (profiles/r1_gemm_dw_layouts.json), for one small transpose.
+        # A producer may hand over Xᵀ it wrote anyway (``xt_given``: the attention output's Oᵀ,
+        # written by the FA2 forward), which makes the token-contiguous dW free for that projection.
+        use_given = (
+            xt_given is not None
+            and xt_given.dtype == cdt
+            and xt_given.shape == (x2.shape[1], x2.shape[0])
+            and xt_given.stride(1) == 1
+        )
+        ctx.xt = x2.is_cuda and any(ctx.needs_input_grad[1:]) and (
+            use_given or _save_transposed(x2.shape[1], w.shape[0]))
         # The input-gradient GEMM dY·W reads W k-strided; from a transposed copy Wᵀ both operands
         # are K-major, which hipBLASLt runs 1.15-1.4x faster (profiles/r1_gemm_dw_layouts.json).
         # Wᵀ is made on the side stream right here, off the forward's critical path.
@@ -384,7 +398,11 @@ class FusedLinearFn(torch.autograd.Function):
             ctx.wt_event.record(s)
         else:
             w_saved = w
-        ctx.save_for_backward(_transpose(x2) if ctx.xt else x2, w_saved)
+        if ctx.xt:
+            x_saved = xt_given if use_given else _transpose(x2)
+        else:
+            x_saved = x2
+        ctx.save_for_backward(x_saved, w_saved)
         ctx.x_shape = x.shape
         ctx.x_dtype = x.dtype
         ctx.rows = [p.shape[0] for p in weights]
@@ -454,11 +472,13 @@ class FusedLinearFn(torch.autograd.Function):
                 dw = _mm_fp32_out(dy2.t(), x2.t() if ctx.xt else x2)
             dw_parts = list(torch.split(dw, ctx.rows, 0))
             dw_parts = [g if g.dtype == dt else g.to(dt) for g, dt in zip(dw_parts, ctx.wdtype)]
-        return (dx, *(dw_parts if dw_parts is not None else [None] * len(ctx.rows)))
+        return (dx, None, *(dw_parts if dw_parts is not None else [None] * len(ctx.rows)))
 
 
-def fused_linear(x: torch.Tensor, *weights: nn.Parameter) -> torch.Tensor:
-    return FusedLinearFn.apply(x, *weights)
+def fused_linear(x: torch.Tensor, *weights: nn.Parameter, xt: torch.Tensor | None = None) -> torch.Tensor:
+    """``x @ [W_0; W_1; ...]^T`` with one GEMM; ``xt`` optionally supplies ``x``'s (K_in, tokens)
+    transpose for the weight gradient (see FusedLinearFn.forward)."""
+    return FusedLinearFn.apply(x, xt, *weights)
 
 
 # ------------------------------------------------------------------------------------------
@@ -485,19 +505,24 @@ class AttentionCore(torch.autograd.Function):
         return qk, t5[:, :, 2].transpose(1, 2)
 
     @staticmethod
-    def forward(ctx, qkv, cos, sin, pos, H):
+    def forward(ctx, qkv, cos, sin, pos, H, want_ot=False):
         qk_in, v = AttentionCore._split(qkv, H)
         hip = _hip()
         qk = hip.rope(qk_in, cos, sin, pos, False)
         q, k = qk[:, :H], qk[:, H:]
         scale = q.shape[-1] ** -0.5
-        o, lse = hip.fa_fwd(q, k, v, True, scale)
+        if want_ot:  # also Oᵀ (H*dk, B*N), the output projection's token-contiguous dW operand
+            o, lse, ot = hip.fa_fwd_ot(q, k, v, True, scale)
+            ctx.mark_non_differentiable(ot)
+        else:
+            o, lse = hip.fa_fwd(q, k, v, True, scale)
+            ot = None
         ctx.save_for_backward(qk, v, o, lse, cos, sin, pos)
         ctx.H, ctx.scale = H, scale
-        return o
+        return o, ot
 
     @staticmethod
-    def backward(ctx, do):
+    def backward(ctx, do, _dot=None):
         qk, v, o, lse, cos, sin, pos = ctx.saved_tensors
         H = ctx.H
         B, N = v.shape[0], v.shape[2]
@@ -508,7 +533,7 @@ class AttentionCore(torch.autograd.Function):
         hip = _hip()
         hip.fa_bwd_into(do, qk[:, :H], qk[:, H:], v, o, lse, True, ctx.scale, dqk[:, :H], dqk[:, H:], dv)
         hip.rope_into(dqk, cos, sin, pos, True, dqk)
-        return dqkv, None, None, None, None
+        return dqkv, None, None, None, None, None
 
 
 class SwiGLUGate(torch.autograd.Function):

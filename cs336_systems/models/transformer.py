@@ -235,7 +235,8 @@ class CausalMultiHeadSelfAttention(nn.Module):
         with annotate("qkv_proj"):
             qkv = fused.fused_linear(x3, *w)  # (B, N, 3*H*dk)
         with annotate("attention"):
-            return fused.AttentionCore.apply(qkv, cos, sin, p, self.num_heads)
+            want_ot = fused.attn_out_transposed() and self.output_proj.weight.requires_grad and torch.is_grad_enabled()
+            return fused.AttentionCore.apply(qkv, cos, sin, p, self.num_heads, want_ot)
 
     def _context_parallel_forward(self, x3, token_positions, B, N):
         """Ring attention over the context-parallel group (``parallel/context_parallel.py``): x3 is
@@ -274,10 +275,15 @@ class CausalMultiHeadSelfAttention(nn.Module):
             with annotate("out_proj"):
                 return self.output_proj(o)
         if x.is_cuda:
-            o = self._fused_path(x3, token_positions, B, N)
-            if o is not None:
+            res = self._fused_path(x3, token_positions, B, N)
+            if res is not None:
+                o, ot = res
                 o = o.transpose(1, 2).reshape(*b, N, H * dk) if b else o.transpose(1, 2).reshape(N, H * dk)
                 with annotate("out_proj"):
+                    op = self.output_proj
+                    if (ot is not None and type(op).forward is Linear.forward and not op._forward_pre_hooks
+                            and not op._forward_hooks):
+                        return fused.fused_linear(o, op.weight, xt=ot)
                     return self.output_proj(o)
         # (B, N, H, dk) memory, viewed as (B, H, N, dk): no transpose copies on the GPU path
         with annotate("qkv_proj"):

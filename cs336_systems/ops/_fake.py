@@ -18,6 +18,12 @@ def _fa_fwd(q, k, v, causal, scale, rope_cos=None, rope_sin=None, rope_pos=None)
     return _bnhd_like(q), q.new_empty((B, H, N), dtype=torch.float32)
 
 
+@register_fake("cs336::fa_fwd_ot")
+def _fa_fwd_ot(q, k, v, causal, scale):
+    B, H, N, D = q.shape
+    return _bnhd_like(q), q.new_empty((B, H, N), dtype=torch.float32), q.new_empty((H * D, B * N))
+
+
 @register_fake("cs336::fa_bwd")
 def _fa_bwd(do, q, k, v, o, lse, causal, scale, rope_cos=None, rope_sin=None, rope_pos=None):
     return _bnhd_like(q), _bnhd_like(k), _bnhd_like(v)

@@ -136,6 +136,28 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
   return {o, lse};
 }
 
+// forward that also writes Oᵀ as a (H*D, B*Nq) token-contiguous matrix (no RoPE-on-load)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_fwd_ot(const at::Tensor& q, const at::Tensor& k,
+                                                         const at::Tensor& v, bool causal, double scale) {
+  check_bhnd(q, "q");
+  check_bhnd(k, "k");
+  check_bhnd(v, "v");
+  TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(), "cs336: q/k/v dtype mismatch");
+  TORCH_CHECK(q.element_size() == 2, "cs336: fa_fwd_ot is 16-bit only");
+  TORCH_CHECK(k.sizes() == v.sizes(), "cs336: k/v shape mismatch");
+  TORCH_CHECK(q.size(0) == k.size(0) && q.size(1) == k.size(1) && q.size(3) == k.size(3), "cs336: q/k shape mismatch");
+  c10::DeviceGuard g(q.device());
+  at::Tensor o = empty_bnhd_like(q);
+  at::Tensor lse = at::empty({q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
+  at::Tensor ot = at::empty({q.size(1) * q.size(3), q.size(0) * q.size(2)}, q.options());
+  cs336::AttnParams p;
+  fill_attn(p, q, k, v, o, lse, causal, scale);
+  p.ot = ot.data_ptr();
+  p.ot_ld = ot.size(1);
+  cs336::flash_attn_fwd(p, to_dtype(q), stream());
+  return {o, lse, ot};
+}
+
 void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                 const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
                 const at::Tensor& dk, const at::Tensor& dv, const OptT& rope_cos, const OptT& rope_sin,
@@ -740,6 +762,7 @@ TORCH_LIBRARY(cs336, m) {
       "adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, "
       "Tensor(d!)[] shadows, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("multi_tensor_l2norm(Tensor[] tensors) -> Tensor");
+  m.def("fa_fwd_ot(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor, Tensor)");
   m.def(
       "adamw_step_t(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, "
       "Tensor(d!)[] shadows, Tensor(e!)[] wts, float lr, float beta1, float beta2, float eps, float weight_decay, "
@@ -750,6 +773,7 @@ TORCH_LIBRARY(cs336, m) {
 
 TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("fa_fwd", &fa_fwd);
+  m.impl("fa_fwd_ot", &fa_fwd_ot);
   m.impl("fa_bwd", &fa_bwd);
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);

@@ -277,6 +277,17 @@ __global__ __launch_bounds__(256, fwd_min_waves<T>()) void fa_fwd_kernel(const A
           store4<T>(orow + d, make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
                                           o[dt][4 * g + 3] * inv));
       }
+    if (p.ot != nullptr) {
+      // Oᵀ: for a fixed d the 32 lanes of a half hold 32 consecutive queries -> 64-B row segments
+      S* ot = (S*)p.ot + (int64_t)h * D * p.ot_ld + (int64_t)b * p.Nq + qrow;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = dt * 32 + 8 * (r >> 2) + 4 * hh + (r & 3);
+          if (DP == D || d < D) ot[(int64_t)d * p.ot_ld] = Elem<T>::from_f(o[dt][r] * inv);
+        }
+    }
     if (hh == 0) p.lse[((int64_t)b * p.H + h) * p.Nq + qrow] = l > 0.f ? (m + __log2f(l)) * kLn2 : -INFINITY;
   }
 }

@@ -129,6 +129,10 @@ struct AttnParams {
   // tile staging by buffer_load ... lds (16-bit, no RoPE-on-load) instead of through VGPRs: bit 0 the
   // forward's K/V tiles, bit 1 the backward's K/V (dQ) and Q/dO (dK/dV) tiles (CS336_FA_DMA, fill_attn)
   int dma = 1;
+  // optional transposed copy of O for the output projection's weight gradient: element (b, h, n, d)
+  // also goes to ot[(h * D + d) * ot_ld + b * Nq + n] (token-contiguous rows, ot_ld = B * Nq)
+  void* ot = nullptr;
+  int64_t ot_ld = 0;
 };
 
 struct AttnBwdParams {

@@ -1,0 +1,45 @@
+"""FA2 forward that also writes Oᵀ (csrc/flash_attn/fa_fwd.hip, `fa_fwd_ot`), consumed as the
+token-contiguous operand of the output projection's weight gradient (models/fused.py)."""
+
+import pytest
+import torch
+
+from cs336_systems import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("D", [64, 80, 128])
+@pytest.mark.parametrize("N", [200, 512])
+def test_fa_fwd_ot_is_transposed_o(D, N):
+    assert ops.load_ext(), ops.load_error()
+    torch.manual_seed(0)
+    B, H = 2, 3
+    mk = lambda: torch.randn(B, N, H, D, device=DEV, dtype=torch.bfloat16).transpose(1, 2)  # noqa: E731
+    q, k, v = mk(), mk(), mk()
+    o, lse = torch.ops.cs336.fa_fwd(q, k, v, True, D**-0.5)
+    o2, lse2, ot = torch.ops.cs336.fa_fwd_ot(q, k, v, True, D**-0.5)
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)
+    # (B, H, N, D) -> (H*D, B*N)
+    ref = o.permute(1, 3, 0, 2).reshape(H * D, B * N)
+    assert ot.shape == (H * D, B * N) and torch.equal(ot, ref)
+
+
+def test_model_grads_with_and_without_ot(monkeypatch):
+    from cs336_systems.models import BasicsTransformerLM
+
+    grads = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CS336_OT", flag)
+        torch.manual_seed(0)
+        m = BasicsTransformerLM(vocab_size=512, context_length=128, d_model=256, num_layers=2, num_heads=4, d_ff=512,
+                                device=DEV)
+        x = torch.randint(0, 512, (4, 128), device=DEV, generator=torch.Generator(DEV).manual_seed(1))
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = ops.cross_entropy(m(x), x)
+        loss.backward()
+        grads.append({n: p.grad.clone() for n, p in m.named_parameters()})
+    for n, g in grads[0].items():
+        scale = g.abs().max().item() + 1e-12
+        torch.testing.assert_close(g / scale, grads[1][n] / scale, rtol=0, atol=2e-3, msg=n)
