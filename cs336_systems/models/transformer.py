@@ -235,7 +235,12 @@ class CausalMultiHeadSelfAttention(nn.Module):
         with annotate("qkv_proj"):
             qkv = fused.fused_linear(x3, *w)  # (B, N, 3*H*dk)
         with annotate("attention"):
-            want_ot = fused.attn_out_transposed() and self.output_proj.weight.requires_grad and torch.is_grad_enabled()
+            want_ot = (
+                fused.attn_out_transposed()
+                and qkv.dtype in (torch.bfloat16, torch.float16)
+                and self.output_proj.weight.requires_grad
+                and torch.is_grad_enabled()
+            )
             return fused.AttentionCore.apply(qkv, cos, sin, p, self.num_heads, want_ot)
 
     def _context_parallel_forward(self, x3, token_positions, B, N):

@@ -277,18 +277,41 @@ __global__ __launch_bounds__(256, fwd_min_waves<T>()) void fa_fwd_kernel(const A
           store4<T>(orow + d, make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
                                           o[dt][4 * g + 3] * inv));
       }
+
+    if (hh == 0) p.lse[((int64_t)b * p.H + h) * p.Nq + qrow] = l > 0.f ? (m + __log2f(l)) * kLn2 : -INFINITY;
+  }
+  if constexpr (!F32) {
     if (p.ot != nullptr) {
-      // Oᵀ: for a fixed d the 32 lanes of a half hold 32 consecutive queries -> 64-B row segments
-      S* ot = (S*)p.ot + (int64_t)h * D * p.ot_ld + (int64_t)b * p.Nq + qrow;
+      // Oᵀ (d-major, queries contiguous) through an LDS transpose: each lane parks its 16-bit outputs at
+      // [d][q] (32 lanes = 32 consecutive queries = 64 B per d), then every d row of the block's 128
+      // queries leaves as 16-B stores (256 B per row)
+      constexpr int LDT = BM + 8;  // padded row (elements)
+      static_assert(DP * LDT * 2 <= NS * 2 * TILE, "Oᵀ staging must fit the K/V ring");
+      S* t = reinterpret_cast<S*>(smem);
+      __syncthreads();  // every wave is done with the K/V ring
+      const int ql = wave * 32 + l32;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int d = dt * 32 + 8 * (r >> 2) + 4 * hh + (r & 3);
-          if (DP == D || d < D) ot[(int64_t)d * p.ot_ld] = Elem<T>::from_f(o[dt][r] * inv);
+          t[d * LDT + ql] = Elem<T>::from_f(o[dt][r] * inv);
         }
+      __syncthreads();
+      S* ot = (S*)p.ot + (int64_t)h * D * p.ot_ld + (int64_t)b * p.Nq + q0;
+      const int nq = min(BM, p.Nq - q0);
+      if ((p.Nq & 7) == 0 && (p.ot_ld & 7) == 0) {
+        for (int c = tid; c < D * (BM / 8); c += 256) {
+          const int d = c / (BM / 8), q8 = 8 * (c % (BM / 8));
+          if (q8 < nq) *reinterpret_cast<uint4*>(ot + (int64_t)d * p.ot_ld + q8) = *reinterpret_cast<const uint4*>(t + d * LDT + q8);
+        }
+      } else {
+        for (int c = tid; c < D * BM; c += 256) {
+          const int d = c / BM, q = c % BM;
+          if (q < nq) ot[(int64_t)d * p.ot_ld + q] = t[d * LDT + q];
+        }
+      }
     }
-    if (hh == 0) p.lse[((int64_t)b * p.H + h) * p.Nq + qrow] = l > 0.f ? (m + __log2f(l)) * kLn2 : -INFINITY;
   }
 }
 
