@@ -24,8 +24,12 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CSRC = os.path.join(ROOT, "csrc")
 OUT_DIR = os.path.dirname(os.path.abspath(__file__))
-OBJ_DIR = os.path.join(OUT_DIR, "obj")
-LIB = os.path.join(OUT_DIR, "libcs336_hip.so")
+# A/B builds of kernel variants: CS336_BUILD_VARIANT=name -DFOO=1 ... builds
+# _native/variants/<name>/libcs336_hip.so with those extra device defines (load it with CS336_LIB=path)
+_VARIANT = os.environ.get("CS336_BUILD_VARIANT", "").split()
+OBJ_DIR = os.path.join(OUT_DIR, "obj") if not _VARIANT else os.path.join(OUT_DIR, "variants", _VARIANT[0], "obj")
+LIB = os.path.join(OUT_DIR, "libcs336_hip.so") if not _VARIANT else os.path.join(OUT_DIR, "variants", _VARIANT[0], "libcs336_hip.so")
+EXTRA_DEFS = _VARIANT[1:]
 ARCH = os.environ.get("CS336_OFFLOAD_ARCH", os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")).split(";")[0]
 
 
@@ -86,7 +90,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
     # -amdgpu-mfma-vgpr-form: keep MFMA accumulators in arch VGPRs (gfx950's file is unified) instead
     # of AGPRs; otherwise hipcc copies every accumulator AGPR<->VGPR around each VALU touch
     # (online-softmax rescale), ~250 v_accvgpr moves per FA tile and half the occupancy.
-    kflags = common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result", *VGPR_FORM]
+    kflags = common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result", *VGPR_FORM, *EXTRA_DEFS]
     if save_temps:
         kflags += ["-save-temps=obj"]
     hflags = common + ["-DUSE_ROCM", "-D__HIP_PLATFORM_AMD__"] + ["-I" + i for i in incs] + [f"--offload-arch={ARCH}"]

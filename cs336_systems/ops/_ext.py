@@ -23,7 +23,8 @@ import torch
 
 _LIB_NAME = "libcs336_hip.so"
 _LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
-LIB_PATH = os.path.join(_LIB_DIR, _LIB_NAME)
+# CS336_LIB: load a variant build instead (A/B runs, cs336_systems/_native/build.py CS336_BUILD_VARIANT)
+LIB_PATH = os.environ.get("CS336_LIB") or os.path.join(_LIB_DIR, _LIB_NAME)
 
 _lock = threading.Lock()
 _loaded: bool | None = None

@@ -21,13 +21,16 @@ namespace fa {
 
 // 16-bit variants ask for two workgroups per CU (<= 256 VGPRs): without the hint the LDS-DMA variant
 // at d 128 took 260 registers, ran one workgroup per CU and lost 37 % (causal, N 4096)
-template <typename T>
+template <typename T, int D>
 constexpr int fwd_min_waves() {
+#ifdef CS336_FA_FWD_WAVES64
+  if (D <= 64 && !std::is_same<T, float>::value) return CS336_FA_FWD_WAVES64;
+#endif
   return std::is_same<T, float>::value ? 1 : 2;
 }
 
 template <typename T, int D, bool CAUSAL, bool ROPE, bool DMA>
-__global__ __launch_bounds__(256, fwd_min_waves<T>()) void fa_fwd_kernel(const AttnParams p) {
+__global__ __launch_bounds__(256, (fwd_min_waves<T, D>())) void fa_fwd_kernel(const AttnParams p) {
   typedef typename Elem<T>::storage S;
   constexpr bool F32 = std::is_same<T, float>::value;
   constexpr int ES = sizeof(S);
