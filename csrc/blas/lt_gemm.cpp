@@ -37,6 +37,8 @@
 #include <hipblaslt/hipblaslt.h>
 #include <torch/library.h>
 
+#include "cs336/tensile_names.h"
+
 #include <algorithm>
 #include <cctype>
 #include <cstdio>
@@ -48,6 +50,9 @@
 #include <vector>
 
 namespace {
+
+using cs336::macro_tile_area;
+using cs336::stream_k_mode;
 
 #define LT_CHECK(expr)                                                                          \
   do {                                                                                          \
@@ -91,18 +96,6 @@ struct Plan {
   std::string kernel;  // Tensile kernel name of the chosen algorithm
 };
 
-// Stream-K mode from a Tensile kernel name: the value of its "SK<n>" token (0 = data-parallel).
-int stream_k_mode(const std::string& name) {
-  size_t pos = 0;
-  while ((pos = name.find("_SK", pos)) != std::string::npos) {
-    size_t i = pos + 3, j = i;
-    while (j < name.size() && std::isdigit(static_cast<unsigned char>(name[j]))) ++j;
-    if (j > i && (j == name.size() || name[j] == '_')) return std::atoi(name.substr(i, j - i).c_str());
-    pos = i;
-  }
-  return 0;
-}
-
 std::string kernel_name(hipblasLtHandle_t h, hipblasLtMatmulAlgo_t& algo) {
   try {
     return hipblaslt_ext::getKernelNameFromAlgo(h, algo);
@@ -144,15 +137,6 @@ hipblasStatus_t launch(hipblasLtHandle_t h, Plan& p, const hipblasLtMatmulAlgo_t
 void run(hipblasLtHandle_t h, Plan& p, const hipblasLtMatmulAlgo_t* algo, const void* a, const void* b, void* out,
          void* ws, size_t ws_bytes, hipStream_t s) {
   LT_CHECK(launch(h, p, algo, a, b, out, ws, ws_bytes, s));
-}
-
-// Macro-tile area from a Tensile kernel name ("..._MT160x256x64_..." -> 160*256), 0 if absent.
-int64_t macro_tile_area(const std::string& name) {
-  const size_t pos = name.find("_MT");
-  if (pos == std::string::npos) return 0;
-  long a = 0, b = 0;
-  if (std::sscanf(name.c_str() + pos + 3, "%ldx%ld", &a, &b) != 2) return 0;
-  return int64_t(a) * int64_t(b);
 }
 
 // The heuristic's top candidates for the big projection GEMMs are all stream-K; enumerate every

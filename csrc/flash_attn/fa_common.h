@@ -62,7 +62,7 @@ struct PadD {
 
 // ---- swizzle: physical 16-B chunk = chunk ^ swz(row) --------------------------------------
 template <int RB>
-__device__ __forceinline__ int swz(int r) {
+__host__ __device__ __forceinline__ int swz(int r) {
   if constexpr (RB == 64) {
     return (r >> 2) & 3;
   } else if constexpr (RB == 192) {
@@ -79,7 +79,7 @@ __device__ __forceinline__ int swz(int r) {
   }
 }
 template <int RB>
-__device__ __forceinline__ int lds_off(int r, int chunk) {
+__host__ __device__ __forceinline__ int lds_off(int r, int chunk) {
   return r * RB + ((chunk ^ swz<RB>(r)) << 4);
 }
 
@@ -310,7 +310,7 @@ __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * 
 // Bijective XCD-aware remap of a 1-D block id: blocks that share a (batch, head) — and hence the
 // same K/V (or Q/dO) stream — become contiguous in the remapped order, i.e. share one XCD's L2
 // (guide T1, bijective variant for totals not divisible by 8).
-__device__ __forceinline__ int xcd_remap(int bid, int total) {
+__host__ __device__ __forceinline__ int xcd_remap(int bid, int total) {
   const int xcd = bid & 7, q = total >> 3, r = total & 7;
   const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   return base + (bid >> 3);
@@ -326,7 +326,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int total) {
 // nbh % 8 == 0 each XCD (bid & 7) keeps a contiguous range of heads, grouped inside the range;
 // otherwise the groups (of 8*grp heads) run over the whole grid. order 2 forces the whole-grid form.
 // Measurements: profiles/r1_fa_lpt_order.md.
-__device__ __forceinline__ void grouped_levels(int j, int nh, int nt, int grp, int& hd, int& lvl) {
+__host__ __device__ __forceinline__ void grouped_levels(int j, int nh, int nt, int grp, int& hd, int& lvl) {
   const int g = grp < nh ? grp : nh;
   const int gi = j / (g * nt), h0 = gi * g;
   const int gs = nh - h0 < g ? nh - h0 : g;  // the last group may be short
@@ -335,7 +335,7 @@ __device__ __forceinline__ void grouped_levels(int j, int nh, int nt, int grp, i
   hd = h0 + r % gs;
 }
 
-__device__ __forceinline__ void tile_order(int bid, int nbh, int nt, int order, int grp, int& bh, int& lvl) {
+__host__ __device__ __forceinline__ void tile_order(int bid, int nbh, int nt, int order, int grp, int& bh, int& lvl) {
   if (order == 1 && (nbh & 7) == 0) {
     const int per = nbh >> 3;
     int hd;
