@@ -180,6 +180,29 @@ def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None =
     return out if out is not None else r
 
 
+def mm_dyt_fp32(dyt: torch.Tensor, x: torch.Tensor, x_is_t: bool, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Weight gradient ``dyt @ x`` (``x_is_t``: ``dyt @ x.T``, x holding Xᵀ) with an fp32 result,
+    from a token-contiguous ``dYᵀ`` (N_out, tokens). hipBLASLt default pick; ``best`` mode also times
+    the autotuned hipBLASLt and the cs336 GEMM (both layouts have a K-major A operand)."""
+    b = x.t() if x_is_t else x
+    if out is None:
+        blas = lambda: torch.mm(dyt, b, out_dtype=torch.float32)  # noqa: E731
+    else:
+        blas = lambda: torch.mm(dyt, b, out_dtype=torch.float32, out=out)  # noqa: E731
+    if _mode() == "blas" or not dyt.is_cuda:
+        r = blas()
+        return out if out is not None else r
+    lt_ok = _lt_ok(dyt, x) and (out is None or out.stride(1) == 1)
+    if out is None:
+        lt = (lambda: ops().lt_gemm(dyt, x, False, x_is_t, torch.float32)) if lt_ok else None
+        cs = (lambda: ops().gemm(dyt, x, False, x_is_t, torch.float32, 0, 0, 0)) if _ok(dyt, x, False, x_is_t) else None
+    else:
+        lt = (lambda: ops().lt_gemm_out(dyt, x, False, x_is_t, out)) if lt_ok else None
+        cs = (lambda: ops().gemm_out(dyt, x, False, x_is_t, out, False, 0, 0, 0)) if _ok(dyt, x, False, x_is_t) else None
+    r = {"blas": blas, "lt": lt, "cs336": cs}[_select("dyt32" + ("t" if x_is_t else "n"), dyt, x, out, blas, lt, cs)]()
+    return out if out is not None else r
+
+
 def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
                concurrent_safe: bool = False) -> torch.Tensor:
     """``dy.T @ x`` with an fp32 result (weight gradient), written into ``out`` when given."""

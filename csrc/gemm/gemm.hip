@@ -40,6 +40,15 @@ typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int kBK = 64;
+
+// Build switches (A/B variants via CS336_BUILD_VARIANT): vectorised LDS-staged epilogue, and
+// s_setprio(1) around each MFMA cluster (cdna_hip_programming.md §5.5 T5).
+#ifndef CS336_GEMM_EPI
+#define CS336_GEMM_EPI 1
+#endif
+#ifndef CS336_GEMM_PRIO
+#define CS336_GEMM_PRIO 0
+#endif
 constexpr int kGroupM = 8;
 
 __device__ __forceinline__ int xcd_remap(int bid, int total) {
@@ -224,10 +233,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, 1) void gemm_kernel(const GemmArgs p
       fb[j] = BKM ? frag_k(ib, wn * WTN + 16 * j, ks, lane) : frag_mn<SB>(ib, wn * WTN + 16 * j, ks, lane);
   };
   auto mma = [&](const bf16x8 (&fa)[FM], const bf16x8 (&fb)[FN]) {
+    if constexpr (CS336_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    if constexpr (CS336_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
   };
   // the wait that retires tile t (loads of t+1 may stay in flight) + the barrier that publishes it
   auto land = [&](int t) {
@@ -296,23 +307,73 @@ __global__ __launch_bounds__(WGM* WGN * 64, 1) void gemm_kernel(const GemmArgs p
 
   // epilogue: lane holds C[4(l>>4)+r][l&15] of each 16x16 block
   const int rbase = m0 + wm * WTM + 4 * (lane >> 4), cbase = n0 + wn * WTN + (lane & 15);
+  constexpr int ES = OUT == 0 ? 2 : 4;  // output element bytes
+  float* cf = reinterpret_cast<float*>(p.c) + (OUT == 0 ? 0 : (int64_t)split * p.split_stride);
+  uint16_t* ch = reinterpret_cast<uint16_t*>(p.c);
+  const bool vec_ok = CS336_GEMM_EPI && ((p.ldc * ES) % 16 == 0) && ((reinterpret_cast<uintptr_t>(p.c) & 15) == 0) &&
+                      ((p.split_stride * ES) % 16 == 0);
+  if (vec_ok) {
+    // Through LDS, one 16-row block of the wave's tile at a time: the accumulators go to a private
+    // [16][WTN] scratch row-major, then come back as 16-B row chunks, so each global store
+    // instruction writes whole 16-B pieces of contiguous rows (the per-lane layout above would
+    // store 2-4 B per lane at a row stride: FM·FN·4 store instructions instead of ~FM·WTN/64).
+    constexpr int RB = WTN * ES, CPR = RB / 16, NCH = 16 * CPR;  // row bytes, chunks per row / block
+    static_assert(RB % 16 == 0, "wave tile row must be whole 16-B chunks");
+    static_assert(NW * 16 * RB <= NS * STAGE, "epilogue scratch exceeds the LDS ring");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();  // every wave's last fragment reads of the ring are done
+    char* scr = smem + wave * 16 * RB;
+    const int r0 = m0 + wm * WTM, c0 = n0 + wn * WTN;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          char* d = scr + (4 * (lane >> 4) + r) * RB + (16 * j + (lane & 15)) * ES;
+          if constexpr (OUT == 0) *reinterpret_cast<uint16_t*>(d) = f2bf(acc[i][j][r]);
+          else *reinterpret_cast<float*>(d) = acc[i][j][r];
+        }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int q0 = 0; q0 < NCH; q0 += 64) {
+        const int q = q0 + lane;
+        if (NCH % 64 == 0 || q < NCH) {
+          const int rr = q / CPR, cc = q % CPR;
+          const uint4 v = *reinterpret_cast<const uint4*>(scr + rr * RB + cc * 16);
+          const int64_t row = r0 + 16 * i + rr;
+          if constexpr (OUT == 0) {
+            *reinterpret_cast<uint4*>(ch + row * p.ldc + c0 + cc * 8) = v;
+          } else {
+            float4* dst = reinterpret_cast<float4*>(cf + row * p.ldc + c0 + cc * 4);
+            float4 f = __builtin_bit_cast(float4, v);
+            if constexpr (OUT == 2) {
+              const float4 o = *dst;
+              f.x += o.x; f.y += o.y; f.z += o.z; f.w += o.w;
+            }
+            *dst = f;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // reads of this block done before the next block's writes
+    }
+    return;
+  }
   if constexpr (OUT == 0) {
-    uint16_t* c = reinterpret_cast<uint16_t*>(p.c);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c[(int64_t)(rbase + 16 * i + r) * p.ldc + cbase + 16 * j] = f2bf(acc[i][j][r]);
+        for (int r = 0; r < 4; ++r) ch[(int64_t)(rbase + 16 * i + r) * p.ldc + cbase + 16 * j] = f2bf(acc[i][j][r]);
   } else {
-    float* c = reinterpret_cast<float*>(p.c) + (int64_t)split * p.split_stride;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float* dst = c + (int64_t)(rbase + 16 * i + r) * p.ldc + cbase + 16 * j;
+          float* dst = cf + (int64_t)(rbase + 16 * i + r) * p.ldc + cbase + 16 * j;
           if constexpr (OUT == 2) *dst += acc[i][j][r];
           else *dst = acc[i][j][r];
         }

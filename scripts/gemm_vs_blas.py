@@ -44,6 +44,8 @@ def main():
             # mixed: only X token-contiguous (saved transposed from the forward) / only dY
             "dw_xt": (lambda: torch.mm(dy.t(), xT.t(), out_dtype=torch.float32), dy, xT, True, True, torch.float32),
             "dw_dyt": (lambda: torch.mm(dyT, x, out_dtype=torch.float32), dyT, x, False, False, torch.float32),
+            # the model's layout: dY and X both token-major (A and B MN-major)
+            "dw": (lambda: torch.mm(dy.t(), x, out_dtype=torch.float32), dy, x, True, False, torch.float32),
         }
         for case, (tfn, a, b, ta, tb, odt) in cases.items():
             M_, N_ = (a.shape[1] if ta else a.shape[0]), (b.shape[0] if tb else b.shape[1])

@@ -80,6 +80,44 @@ def main():
             print(f"| {k} | {n[k]} | {ms:.1f} | {ach:.2f} TB/s | {PEAK_TBS} TB/s HBM | {100 * ach / PEAK_TBS:.0f} % |")
         else:
             print(f"| {k} | {n[k]} | {ms:.1f} | | | |")
+    gemm_roles(step, xf, M, d, f, L, V)
+
+
+def gemm_roles(step, xf, M, d, f, L, V):
+    """Per-projection GEMM times, labelled by the step's fixed launch order: forward = L x (qkv, o,
+    w13, w2) + lm head; backward = lm head (dX, dW), then per layer in reverse w2, w13, o, qkv, each
+    dX then dW. Only printed when the GEMM counts match that order (no side-stream reordering)."""
+    g = [(s, e, k) for s, e, k in step if k.startswith("Cijk") or k.startswith("Custom_Cijk")]
+    fwd = [x for x in g if x[0] < xf]
+    bwd = [x for x in g if x[0] >= xf]
+    if len(fwd) != 4 * L + 1 or len(bwd) != 8 * L + 2:
+        print(f"\n(GEMM order not recognised: {len(fwd)} fwd / {len(bwd)} bwd GEMMs)")
+        return
+    flops = {"qkv": 2 * M * d * 3 * d, "o": 2 * M * d * d, "w13": 2 * M * d * 2 * f, "w2": 2 * M * f * d, "lm": 2 * M * d * V}
+    t = defaultdict(float)
+    names = {}
+    for i, (s, e, k) in enumerate(fwd[:-1]):
+        role = ("qkv", "o", "w13", "w2")[i % 4] + " fwd"
+        t[role] += (e - s) / 1e6
+        names[role] = k
+    t["lm fwd"] += (fwd[-1][1] - fwd[-1][0]) / 1e6
+    names["lm fwd"] = fwd[-1][2]
+    for j, (s, e, k) in enumerate(bwd):
+        if j < 2:
+            role = "lm " + ("dX", "dW")[j]
+        else:
+            role = ("w2", "w13", "o", "qkv")[((j - 2) // 2) % 4] + " " + ("dX", "dW")[(j - 2) % 2]
+        t[role] += (e - s) / 1e6
+        names[role] = k
+    print("\n| GEMM | ms/step | us/call | TFLOP/s | kernel (last call) |")
+    print("|---|---|---|---|---|")
+    for role, ms in sorted(t.items(), key=lambda x: -x[1]):
+        proj = role.split()[0]
+        calls = 1 if proj == "lm" else L
+        tf = flops[proj] * calls / (ms * 1e-3) / 1e12
+        tile = re.search(r"MT\d+x\d+x\d+", names[role])
+        sk = "SK" if "_SK" in names[role] else ""
+        print(f"| {role} | {ms:.2f} | {1000 * ms / calls:.1f} | {tf:.0f} | {tile.group(0) if tile else names[role][:30]} {sk} |")
 
 
 if __name__ == "__main__":
