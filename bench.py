@@ -354,6 +354,13 @@ def main(argv=None):
         import torch.cuda.tunable as tunable
 
         log(f"TunableOp results are written to {tunable.get_filename()} at exit")
+    rep = os.environ.get("CS336_GEMM_REPORT")
+    if rep and rank == 0 and gemm_mode() == "best":  # per-problem candidate times of best mode
+        from cs336_systems.ops.gemm import gemm_choices, gemm_timings
+
+        ch = gemm_choices()
+        with open(rep, "w") as fh:
+            json.dump([{"key": str(k), "pick": ch.get(k), "ms": v} for k, v in gemm_timings().items()], fh, indent=1)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

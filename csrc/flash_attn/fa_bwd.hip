@@ -32,6 +32,9 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   constexpr int ES = sizeof(S);
   constexpr int DP = PadD<D>::value;  // compute width (80 -> 96; d >= D is zero, never loaded/stored)
   constexpr int RB = DP * ES, CPR = RB / 16, EPC = 16 / ES, CREAL = D * ES / 16;
+  // -delta as the dP accumulators' initial value (+1-2 % at d64/d128); at the padded d80 the extra
+  // live row constants cost more than the saved subtraction (-17 %), so it keeps the explicit form
+  constexpr bool DINIT = DP == D;
   // D=128 streams 32-key tiles: halves the S^T/dP^T/staging registers so the kernel fits 256
   // VGPRs without spilling (64-key tiles spilled at occupancy 1)
   constexpr int BM = 128, BN = DP == 128 ? 32 : 64;
@@ -141,7 +144,10 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         s[t] = zero16();
-        dp[t] = zero16();
+        // row constant as the initial accumulator: dP' = dO V^T - delta[q] leaves the chain ready
+        // for dS = P dP' (one VALU op per element fewer; the query is on the lane)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dp[t][r] = DINIT ? -delta : 0.f;
         if constexpr (F32) {
 #pragma unroll
           for (int i = 0; i < DP / 8; ++i) {
@@ -176,7 +182,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
             const int key = kt0 + 32 * t + acc_row(r, hh);
             if (key >= p.Nk || (CAUSAL && key > qrow)) pv = 0.f;
           }
-          s[t][r] = pv * (dp[t][r] - delta);  // dS^T
+          s[t][r] = DINIT ? pv * dp[t][r] : pv * (dp[t][r] - delta);  // dS^T
         }
       if constexpr (F32) {
 #pragma unroll
@@ -288,6 +294,9 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
   constexpr int ES = sizeof(S);
   constexpr int DP = PadD<D>::value;  // compute width (80 -> 96; d >= D is zero, never loaded/stored)
   constexpr int RB = DP * ES, CPR = RB / 16, EPC = 16 / ES, CREAL = D * ES / 16;
+  // -delta as the dP accumulators' initial value (+1-2 % at d64/d128); at the padded d80 the extra
+  // live row constants cost more than the saved subtraction (-17 %), so it keeps the explicit form
+  constexpr bool DINIT = DP == D;
   // 64-query tiles; at D=128 (one workgroup per CU anyway) part of the state lives in AGPRs
   // rather than halving the tile: 1153 -> 1046 us at N=4096 (fp32 keeps 32-query tiles)
   constexpr int BK = 128, BQ = (D == 128 && std::is_same<T, float>::value) ? 32 : 64;
@@ -409,7 +418,19 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         s[t] = zero16();
-        dp[t] = zero16();
+        // dP accumulators start at -delta[q] (row constants per register): dS = P dP' afterwards
+        if constexpr (DINIT) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float4 D4 = *reinterpret_cast<const float4*>(Ds + 32 * t + 8 * g + 4 * hh);
+            dp[t][4 * g] = -D4.x;
+            dp[t][4 * g + 1] = -D4.y;
+            dp[t][4 * g + 2] = -D4.z;
+            dp[t][4 * g + 3] = -D4.w;
+          }
+        } else {
+          dp[t] = zero16();
+        }
         if constexpr (F32) {
 #pragma unroll
           for (int i = 0; i < DP / 8; ++i) {
@@ -442,8 +463,9 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
         for (int g = 0; g < 4; ++g) {
           const int qr = 32 * t + 8 * g + 4 * hh;
           const float4 L4 = *reinterpret_cast<const float4*>(Ls + qr);
-          const float4 D4 = *reinterpret_cast<const float4*>(Ds + qr);
           const float Lv[4] = {L4.x, L4.y, L4.z, L4.w};
+          float4 D4 = make_float4(0.f, 0.f, 0.f, 0.f);
+          if constexpr (!DINIT) D4 = *reinterpret_cast<const float4*>(Ds + qr);
           const float Dv[4] = {D4.x, D4.y, D4.z, D4.w};
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
@@ -451,7 +473,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
             float pv = fexp2(fmaf(s[t][r], c2, -Lv[u] * lscale));
             if (need_mask && ((CAUSAL && krow > qt0 + qr + u) || (DMA && qt0 + qr + u >= p.Nq))) pv = 0.f;
             s[t][r] = pv;
-            dp[t][r] = pv * (dp[t][r] - Dv[u]);
+            dp[t][r] = DINIT ? pv * dp[t][r] : pv * (dp[t][r] - Dv[u]);
           }
         }
       if constexpr (F32) {
