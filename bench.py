@@ -57,6 +57,12 @@ def parse(argv=None):
         help="zero = ZeRO-2: reduce-scattered grads, sharded fused AdamW, param all-gather under the next forward",
     )
     ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument(
+        "--grad-comm-dtype",
+        default="fp32",
+        choices=["fp32", "bf16"],
+        help="bucketed DDP: dtype of the gradients on the wire (bf16 halves the all-reduce bytes)",
+    )
     ap.add_argument("--sharded", action="store_true", help="ZeRO-1 sharded optimizer state")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--lr", type=float, default=1e-4)
@@ -125,6 +131,9 @@ def dist_diagnostics(ddp_model, comm_wait_ms, device, world) -> dict:
         d["n_buckets"] = len(mbs)
         d["bucket_mb"] = {"min": round(min(mbs), 2), "max": round(max(mbs), 2), "total": round(sum(mbs), 1)}
         d["bucket_sizes_mb"] = [round(m, 1) for m in mbs]
+        if "wire_mb" in buckets[0]:
+            d["wire_dtype"] = buckets[0]["wire"]
+            d["wire_mb_total"] = round(sum(b["wire_mb"] for b in buckets), 1)
     try:
         v = torch.cuda.nccl.version()
         d["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
@@ -193,7 +202,8 @@ def main(argv=None):
     if zero:
         ddp_model = ZeroDDP(model, bucket_size_mb=bucket, bf16_shadows=shadows, **okw)
     elif world > 1:
-        ddp_model = wrap_ddp(model, args.ddp, bucket_size_mb=bucket)
+        kw = {"comm_dtype": torch.bfloat16} if args.grad_comm_dtype == "bf16" and args.ddp == "bucketed" else {}
+        ddp_model = wrap_ddp(model, args.ddp, bucket_size_mb=bucket, **kw)
     else:
         ddp_model = model
     overlap = args.overlap_opt == "on" or (
@@ -329,6 +339,7 @@ def main(argv=None):
             "parallelism": f"dp{world}" + ("+zero2" if zero else "+zero1" if args.sharded and world > 1 else ""),
             "ddp": args.ddp if world > 1 or zero else "none",
             "bucket_mb": bucket if world > 1 or zero else None,
+            "grad_comm_dtype": args.grad_comm_dtype if world > 1 and args.ddp == "bucketed" and not zero else None,
             "optimizer": "fused HIP AdamW (fp32 master weights)"
             + (", overlapped with backward" if overlap else "")
             + (", sharded 1/W with param all-gather under the forward" if zero else ""),

@@ -217,6 +217,8 @@ class FusedAdamW(torch.optim.Optimizer):
             return self._ov is not None
         if ddp is not None and not (hasattr(ddp, "add_bucket_callback") and getattr(ddp, "_avg", False)):
             return False
+        if ddp is not None and hasattr(ddp, "supports_bucket_callbacks") and not ddp.supports_bucket_callbacks():
+            return False
         ov = _Overlap(params[0].device, max(1, int(chunk_mb * 2**20 / 4)))
         self._group_of = {id(p): g for g in self.param_groups for p in g["params"]}
         if ddp is not None:

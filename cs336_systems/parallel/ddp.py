@@ -201,12 +201,13 @@ class DDPIndividual(_DDPBase):
 
 
 class _Bucket:
-    __slots__ = ("idx", "params", "flat", "pending", "handle", "launched")
+    __slots__ = ("idx", "params", "flat", "cflat", "pending", "handle", "launched")
 
-    def __init__(self, idx: int, params: list, flat: torch.Tensor):
+    def __init__(self, idx: int, params: list, flat: torch.Tensor, cflat: torch.Tensor | None = None):
         self.idx = idx
         self.params = params
         self.flat = flat
+        self.cflat = cflat  # low-precision wire copy (comm_dtype), or None
         self.pending = len(params)
         self.handle = None
         self.launched = False
@@ -222,11 +223,22 @@ class DDPBucketed(_DDPBase):
     resets grads to ``None`` (``optimizer.zero_grad()``), the projection GEMMs of the model write
     their fp32 dW directly into the bucket (``p._cs336_grad_out``; no memset, no accumulate add,
     no copy) and any other fresh gradient is copied into its view once by the hook.
+
+    ``comm_dtype`` (e.g. ``torch.bfloat16``) puts the gradients on the wire in that dtype: each
+    bucket is cast into a persistent wire buffer when it is issued, reduced there (AVG on RCCL),
+    and cast back into the fp32 bucket at ``finish_gradient_synchronization``. Half the bytes per
+    xGMI link for bf16 (the all-reduce is link-bound: 8 GB of fp32 gradients per GPT-2-XL step),
+    for two extra elementwise passes over the bucket and bf16 rounding of the sum (the gradients
+    themselves are already products of bf16 GEMM operands under autocast). Not combinable with the
+    optimizer's per-bucket overlap callbacks (the reduced values reach the fp32 bucket only at
+    finish). Default ``None``: the bucket's own dtype, as in the reference.
     """
 
-    def __init__(self, module: nn.Module, bucket_size_mb: float | None = DEFAULT_BUCKET_MB, process_group=None, broadcast: bool = True):
+    def __init__(self, module: nn.Module, bucket_size_mb: float | None = DEFAULT_BUCKET_MB, process_group=None,
+                 broadcast: bool = True, comm_dtype: torch.dtype | None = None):
         super().__init__(module, process_group, broadcast)
         self.bucket_size_mb = bucket_size_mb
+        self.comm_dtype = comm_dtype
         cap = float("inf") if bucket_size_mb is None else bucket_size_mb * 1024 * 1024
         params = [p for p in _unique_params(module) if p.requires_grad]
         groups = bucket_params(params, cap)
@@ -240,7 +252,10 @@ class DDPBucketed(_DDPBase):
                 self._views[p] = flat[off : off + p.numel()].view_as(p)
                 self._param_bucket[p] = None  # filled below
                 off += p.numel()
-            b = _Bucket(i, ps, flat)
+            wire = None
+            if comm_dtype is not None and comm_dtype != flat.dtype:
+                wire = torch.empty(flat.numel(), device=flat.device, dtype=comm_dtype)
+            b = _Bucket(i, ps, flat, wire)
             self.buckets.append(b)
             for p in ps:
                 self._param_bucket[p] = b
@@ -257,7 +272,12 @@ class DDPBucketed(_DDPBase):
         """``fn(params, work)`` runs right after a bucket's all-reduce is issued (``work`` is its
         async handle; with AVG the reduced gradients are final once it completes). Used by
         :class:`~cs336_systems.ops.FusedAdamW` to update each bucket during backward."""
+        if any(b.cflat is not None for b in self.buckets):
+            raise RuntimeError("per-bucket callbacks need full-precision buckets (comm_dtype=None)")
         self._bucket_callbacks.append(fn)
+
+    def supports_bucket_callbacks(self) -> bool:
+        return self._avg and all(b.cflat is None for b in self.buckets)
 
     # ---- grad buffer management -------------------------------------------------------------
     def zero_grad(self, set_to_none: bool = False) -> None:
@@ -285,7 +305,11 @@ class DDPBucketed(_DDPBase):
             self._issued.clear()
         self._issued.append(b.idx)
         with annotate(f"comm.bucket{b.idx}"):
-            b.handle = self._all_reduce(b.flat, async_op=True)
+            if b.cflat is not None:
+                self._cast_into(b.cflat, b.flat)
+                b.handle = self._all_reduce(b.cflat, async_op=True)
+            else:
+                b.handle = self._all_reduce(b.flat, async_op=True)
         b.launched = True
         for fn in self._bucket_callbacks:
             fn(b.params, b.handle)
@@ -309,10 +333,24 @@ class DDPBucketed(_DDPBase):
         self._next = 0
         for b in self.buckets:
             b.handle.wait()
+            if b.cflat is not None:
+                b.flat.copy_(b.cflat)
             self._finish_mean(b.flat)
             b.handle = None
             b.launched = False
             b.pending = len(b.params)
+
+    @staticmethod
+    def _cast_into(dst: torch.Tensor, src: torch.Tensor) -> None:
+        """dst <- src (dtype cast) on the stream that may still be writing src (the dW side
+        stream), else on the current stream."""
+        side = dw_stream_for(src)
+        if side is None:
+            dst.copy_(src)
+            return
+        side.wait_stream(torch.cuda.current_stream(src.device))
+        with torch.cuda.stream(side):
+            dst.copy_(src)
 
     def launch_order(self) -> list[int]:
         """Bucket indices in the order their collectives were issued last step (tests)."""
@@ -320,7 +358,10 @@ class DDPBucketed(_DDPBase):
 
     def bucket_summary(self) -> list[dict]:
         return [
-            dict(bucket=b.idx, n_params=len(b.params), mb=b.flat.numel() * b.flat.element_size() / 2**20)
+            dict(bucket=b.idx, n_params=len(b.params), mb=b.flat.numel() * b.flat.element_size() / 2**20,
+                 wire=str(b.cflat.dtype if b.cflat is not None else b.flat.dtype).replace("torch.", ""),
+                 wire_mb=(b.cflat if b.cflat is not None else b.flat).numel()
+                 * (b.cflat if b.cflat is not None else b.flat).element_size() / 2**20)
             for b in self.buckets
         ]
 

@@ -27,7 +27,10 @@ def _run(nproc: int, *extra: str) -> list[dict]:
     return [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
 
 
-@pytest.mark.parametrize("nproc,extra", [(2, ()), (4, ()), (2, ("--sharded",)), (2, ("--ddp", "zero"))])
+@pytest.mark.parametrize(
+    "nproc,extra",
+    [(2, ()), (4, ()), (2, ("--sharded",)), (2, ("--ddp", "zero")), (2, ("--grad-comm-dtype", "bf16"))],
+)
 def test_bench_multirank_json(nproc, extra):
     lines = _run(nproc, *extra)
     assert len(lines) == 1, lines
@@ -48,3 +51,6 @@ def test_bench_multirank_json(nproc, extra):
     assert dd["n_buckets"] == len(dd["bucket_sizes_mb"]) >= 1
     assert dd["bucket_mb"]["max"] <= 128.0 + 1e-6
     assert "rccl_version" in dd and isinstance(dd["env"], dict)
+    if "--grad-comm-dtype" in extra:
+        assert d["config"]["grad_comm_dtype"] == "bf16" and dd["wire_dtype"] == "bfloat16"
+        assert dd["wire_mb_total"] == pytest.approx(dd["bucket_mb"]["total"] / 2, rel=0.01)

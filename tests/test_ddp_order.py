@@ -148,3 +148,37 @@ def _fused_residual_worker(rank, world):
 @pytest.mark.timeout(120)
 def test_zero_fused_residual_waits_for_gathers():
     spawn(_fused_residual_worker, 2)
+
+
+def _wire_bf16_worker(rank, world):
+    """DDPBucketed(comm_dtype=bf16): gradients cross the wire in bf16 and land back in the fp32
+    buckets as the mean over ranks, to bf16 rounding; the bucket order is unchanged."""
+    _init(rank, world)
+    torch.manual_seed(0)
+    model = RankGatedModel()
+    ref = RankGatedModel()
+    ref.load_state_dict(model.state_dict())
+    wrapped = DDPBucketed(model, bucket_size_mb=0.0005, comm_dtype=torch.bfloat16)
+    assert all(b.cflat is not None and b.cflat.dtype == torch.bfloat16 for b in wrapped.buckets)
+    assert {b["wire"] for b in wrapped.bucket_summary()} == {"bfloat16"}
+    with pytest.raises(RuntimeError):
+        wrapped.add_bucket_callback(lambda ps, w: None)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(world * 4, 8, generator=g)
+    y = torch.randn(world * 4, 4, generator=g)
+    loss = sum(F.mse_loss(ref(x[r * 4 : (r + 1) * 4], r == 0), y[r * 4 : (r + 1) * 4]) for r in range(world)) / world
+    loss.backward()
+    xs, ys = x[rank * 4 : (rank + 1) * 4], y[rank * 4 : (rank + 1) * 4]
+    F.mse_loss(wrapped.module(xs, rank == 0), ys).backward()
+    wrapped.finish_gradient_synchronization()
+    assert wrapped.launch_order() == list(range(len(wrapped.buckets)))
+    for (n, p), q in zip(model.named_parameters(), ref.parameters()):
+        assert p.grad.dtype == torch.float32
+        torch.testing.assert_close(p.grad, q.grad, rtol=2e-2, atol=1e-3, msg=lambda m, n=n: f"{n}: {m}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_bf16_gradient_wire():
+    spawn(_wire_bf16_worker, 2)
