@@ -61,7 +61,7 @@ def parse(argv=None):
         "--grad-comm-dtype",
         default="fp32",
         choices=["fp32", "bf16"],
-        help="bucketed DDP: dtype of the gradients on the wire (bf16 halves the all-reduce bytes)",
+        help="bucketed DDP / ZeRO-2: dtype of the gradients on the wire (bf16 halves the all-reduce / reduce-scatter bytes)",
     )
     ap.add_argument("--sharded", action="store_true", help="ZeRO-1 sharded optimizer state")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -200,7 +200,8 @@ def main(argv=None):
     shadows = amp and not args.no_shadows
     bucket = args.bucket_mb if args.bucket_mb is not None else DEFAULT_BUCKET_MB
     if zero:
-        ddp_model = ZeroDDP(model, bucket_size_mb=bucket, bf16_shadows=shadows, **okw)
+        zkw = {"comm_dtype": torch.bfloat16} if args.grad_comm_dtype == "bf16" else {}
+        ddp_model = ZeroDDP(model, bucket_size_mb=bucket, bf16_shadows=shadows, **zkw, **okw)
     elif world > 1:
         kw = {"comm_dtype": torch.bfloat16} if args.grad_comm_dtype == "bf16" and args.ddp == "bucketed" else {}
         ddp_model = wrap_ddp(model, args.ddp, bucket_size_mb=bucket, **kw)
@@ -339,7 +340,7 @@ def main(argv=None):
             "parallelism": f"dp{world}" + ("+zero2" if zero else "+zero1" if args.sharded and world > 1 else ""),
             "ddp": args.ddp if world > 1 or zero else "none",
             "bucket_mb": bucket if world > 1 or zero else None,
-            "grad_comm_dtype": args.grad_comm_dtype if world > 1 and args.ddp == "bucketed" and not zero else None,
+            "grad_comm_dtype": args.grad_comm_dtype if world > 1 and (args.ddp == "bucketed" or zero) else None,
             "optimizer": "fused HIP AdamW (fp32 master weights)"
             + (", overlapped with backward" if overlap else "")
             + (", sharded 1/W with param all-gather under the forward" if zero else ""),

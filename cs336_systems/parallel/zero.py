@@ -42,7 +42,7 @@ from .ddp import DEFAULT_BUCKET_MB, _unique_params, bucket_params
 
 class _ZBucket:
     __slots__ = ("idx", "params", "pbuf", "gbuf", "sbuf", "shard", "gshard", "master", "staged", "pending",
-                 "launched", "rs", "ag", "bf16")
+                 "launched", "rs", "ag", "bf16", "wbuf", "wshard")
 
     def __init__(self, idx, params, pbuf, gbuf, sbuf, shard, gshard, master, staged, bf16=False):
         self.idx, self.params, self.pbuf, self.gbuf, self.sbuf = idx, params, pbuf, gbuf, sbuf
@@ -53,6 +53,7 @@ class _ZBucket:
         self.launched = False
         self.rs = None  # reduce-scatter work
         self.ag = None  # param all-gather work (True: a completed host-staged gather)
+        self.wbuf = self.wshard = None  # low-precision wire copies of gbuf / gshard (comm_dtype)
 
 
 class _ZeroAdamW(FusedAdamW):
@@ -98,6 +99,7 @@ class ZeroDDP(nn.Module):
         bf16_shadows: bool = False,
         overlap_param_gather: bool = True,
         gather_dtype: str = "auto",
+        comm_dtype: torch.dtype | None = None,
         _collectives_at_world1: bool = False,
     ):
         super().__init__()
@@ -169,6 +171,11 @@ class ZeroDDP(nn.Module):
                 elif b16:  # the update kernel writes this rank's shadow slice; the gather ships it
                     setattr(master, _SHADOW, sbuf[r * shard : (r + 1) * shard])
                 b = _ZBucket(i, ps, pbuf, gbuf, sbuf, shard, gshard, master, self._gloo and dev.type == "cuda", b16)
+                if comm_dtype is not None and comm_dtype != torch.float32 and not self._solo:
+                    # gradients reduce-scattered in comm_dtype (half the bytes for bf16), cast back
+                    # into the fp32 shard the update reads at finish_gradient_synchronization
+                    b.wbuf = torch.empty(shard * W, device=dev, dtype=comm_dtype)
+                    b.wshard = torch.empty(shard, device=dev, dtype=comm_dtype)
                 self.buckets.append(b)
                 for p in ps:
                     self._param_bucket[p] = b
@@ -241,20 +248,26 @@ class ZeroDDP(nn.Module):
         with annotate(f"comm.rs{b.idx}"):
             if b.staged:  # gloo cannot reduce-scatter HIP tensors: stage on the host
                 sync_dw_stream()
-                out = torch.empty(b.shard, dtype=torch.float32)
-                dist.reduce_scatter_tensor(out, b.gbuf.cpu(), op=op, group=self.process_group)
+                wdt = b.wbuf.dtype if b.wbuf is not None else torch.float32
+                out = torch.empty(b.shard, dtype=wdt)
+                dist.reduce_scatter_tensor(out, b.gbuf.to(wdt).cpu(), op=op, group=self.process_group)
                 b.gshard.copy_(out)
                 return
+            src, dst = (b.gbuf, b.gshard) if b.wbuf is None else (b.wbuf, b.wshard)
             side = dw_stream_for(b.gbuf)
             if side is None:
-                b.rs = dist.reduce_scatter_tensor(b.gshard, b.gbuf, op=op, group=self.process_group, async_op=True)
+                if b.wbuf is not None:
+                    b.wbuf.copy_(b.gbuf)
+                b.rs = dist.reduce_scatter_tensor(dst, src, op=op, group=self.process_group, async_op=True)
                 return
             # weight gradients may still be in flight on the dW side stream: issue from that stream
             # once it has caught up with the main stream (as DDPBucketed._all_reduce), so the main
             # stream keeps running backward instead of waiting for every dW GEMM issued so far
             side.wait_stream(torch.cuda.current_stream(b.gbuf.device))
             with torch.cuda.stream(side):
-                b.rs = dist.reduce_scatter_tensor(b.gshard, b.gbuf, op=op, group=self.process_group, async_op=True)
+                if b.wbuf is not None:
+                    b.wbuf.copy_(b.gbuf)
+                b.rs = dist.reduce_scatter_tensor(dst, src, op=op, group=self.process_group, async_op=True)
 
     def launch_order(self) -> list[int]:
         """Bucket indices in the order their reduce-scatters were issued last step (tests)."""
@@ -270,6 +283,8 @@ class ZeroDDP(nn.Module):
             if b.rs is not None:
                 b.rs.wait()
                 b.rs = None
+                if b.wshard is not None:
+                    b.gshard.copy_(b.wshard)
             if not self._avg and self.world_size > 1:
                 b.gshard.div_(self.world_size)
             b.launched = False
@@ -376,4 +391,7 @@ class ZeroDDP(nn.Module):
 
     def bucket_summary(self) -> list[dict]:
         return [dict(bucket=b.idx, n_params=len(b.params), mb=b.pbuf.numel() * 4 / 2**20, shard=b.shard,
-                     gather="bf16" if b.bf16 else "fp32") for b in self.buckets]
+                     gather="bf16" if b.bf16 else "fp32",
+                     wire=str(b.wbuf.dtype if b.wbuf is not None else torch.float32).replace("torch.", ""),
+                     wire_mb=b.pbuf.numel() * (b.wbuf.element_size() if b.wbuf is not None else 4) / 2**20)
+                for b in self.buckets]

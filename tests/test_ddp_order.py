@@ -182,3 +182,37 @@ def _wire_bf16_worker(rank, world):
 @pytest.mark.timeout(120)
 def test_bf16_gradient_wire():
     spawn(_wire_bf16_worker, 2)
+
+
+def _zero_wire_bf16_worker(rank, world):
+    """ZeroDDP(comm_dtype=bf16): each rank's fp32 gradient shard is the bf16-reduced mean."""
+    _init(rank, world)
+    torch.manual_seed(0)
+    model = RankGatedModel()
+    ref = RankGatedModel()
+    ref.load_state_dict(model.state_dict())
+    wrapped = ZeroDDP(model, bucket_size_mb=0.0005, comm_dtype=torch.bfloat16, **OPT)
+    assert {b["wire"] for b in wrapped.bucket_summary()} == {"bfloat16"}
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(world * 4, 8, generator=g)
+    y = torch.randn(world * 4, 4, generator=g)
+    loss = sum(F.mse_loss(ref(x[r * 4 : (r + 1) * 4], r == 0), y[r * 4 : (r + 1) * 4]) for r in range(world)) / world
+    loss.backward()
+    wrapped.zero_grad(set_to_none=True)
+    xs, ys = x[rank * 4 : (rank + 1) * 4], y[rank * 4 : (rank + 1) * 4]
+    F.mse_loss(wrapped.module(xs, rank == 0), ys).backward()
+    wrapped.finish_gradient_synchronization()
+    refp = dict(zip([id(p) for p in model.parameters()], ref.parameters()))
+    for b in wrapped.buckets:
+        flat = torch.cat([refp[id(p)].grad.reshape(-1) for p in b.params])
+        flat = torch.nn.functional.pad(flat, (0, b.shard * world - flat.numel()))
+        want = flat[rank * b.shard : (rank + 1) * b.shard]
+        assert b.gshard.dtype == torch.float32
+        torch.testing.assert_close(b.gshard, want, rtol=2e-2, atol=1e-3)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_zero_bf16_gradient_wire():
+    spawn(_zero_wire_bf16_worker, 2)
