@@ -333,6 +333,31 @@ def _dy_transposed(k_in: int, n_out: int) -> bool:
     return os.environ.get("CS336_DYT", "1") != "0" and n_out <= k_in
 
 
+# Transposed bf16 gradients written by their producer (the fused residual RMSNorm backward) for
+# the weight-gradient GEMM of the projection that consumes the row-major copy: keyed by the row-major
+# tensor's data pointer; the entry holds that tensor, so its storage (and address) cannot be reused
+# while the entry lives. At most a few entries (an unconsumed offer is dropped oldest-first).
+_DYT_OFFERS: "dict[int, tuple[torch.Tensor, torch.Tensor]]" = {}
+
+
+def offer_transposed_grad(g: torch.Tensor, gt: torch.Tensor) -> None:
+    _DYT_OFFERS[g.data_ptr()] = (g, gt)
+    while len(_DYT_OFFERS) > 4:
+        _DYT_OFFERS.pop(next(iter(_DYT_OFFERS)))
+
+
+def take_transposed_grad(g2: torch.Tensor) -> torch.Tensor | None:
+    """The producer-written ``g2ᵀ`` for a 2-D row-major gradient ``g2`` (same storage, same
+    element count, same dtype), or None."""
+    e = _DYT_OFFERS.pop(g2.data_ptr(), None)
+    if e is None:
+        return None
+    g, gt = e
+    ok = (g.numel() == g2.numel() and g.dtype == g2.dtype and g2.is_contiguous()
+          and gt.shape == (g2.shape[1], g2.shape[0]) and gt.dtype == g2.dtype)
+    return gt if ok else None
+
+
 def attn_out_transposed() -> bool:
     """The FA2 forward also writes Oᵀ for the output projection's weight gradient (CS336_OT=0: off)."""
     return os.environ.get("CS336_OT", "1") != "0"
@@ -462,7 +487,9 @@ class FusedLinearFn(torch.autograd.Function):
             )
             dyt = None
             if not side and dy2.is_cuda and dy2.dtype == torch.bfloat16 and _dy_transposed(ctx.x_shape[-1], dy2.shape[1]):
-                dyt = _transpose(dy2)
+                dyt = take_transposed_grad(dy2)
+                if dyt is None:
+                    dyt = _transpose(dy2)
             if dyt is not None:  # dYᵀ (N_out, tokens); x2 is X or Xᵀ
                 dw_fn = lambda out=None, cs=False: gemm.mm_dyt_fp32(dyt, x2, ctx.xt, out=out)  # noqa: E731
             elif ctx.xt:  # x2 holds Xᵀ (K_in, tokens)

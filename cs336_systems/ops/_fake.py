@@ -62,6 +62,13 @@ def _rms_bwd_add(dy, x, w, rstd, dres, emit_bf16):
     return torch.empty_like(x), dx2, w.new_empty(w.shape, dtype=torch.float32)
 
 
+@register_fake("cs336::rmsnorm_bwd_add_t")
+def _rms_bwd_add_t(dy, x, w, rstd, dres, emit_bf16):
+    dx2 = x.new_empty(x.shape if emit_bf16 else (0,), dtype=torch.bfloat16)
+    dxt = x.new_empty((x.shape[1], x.shape[0]), dtype=torch.bfloat16)
+    return torch.empty_like(x), dx2, dxt, w.new_empty(w.shape, dtype=torch.float32)
+
+
 @register_fake("cs336::rope")
 def _rope(x, cos, sin, pos, inverse):
     return _bnhd_like(x)

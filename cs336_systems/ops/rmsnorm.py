@@ -77,9 +77,27 @@ class AddRMSNormHIP(torch.autograd.Function):
             if not ds2.is_contiguous() or ds2.dtype != s.dtype:
                 ds2 = ds2.contiguous().to(s.dtype)
             emit = ctx.r_dtype == torch.bfloat16 and s.dtype != torch.bfloat16
-            dx, dx_bf16, dw = ops().rmsnorm_bwd_add(dy2, s, weight, rstd, ds2, emit)
+            if emit and _want_transposed_grad(s):
+                # the branch is a narrow projection whose dW takes dYᵀ (models/fused.py): write it
+                # here, transposed through LDS, instead of a separate transpose of dr
+                dx, dx_bf16, dxt, dw = ops().rmsnorm_bwd_add_t(dy2, s, weight, rstd, ds2, True)
+                from ..models.fused import offer_transposed_grad
+
+                offer_transposed_grad(dx_bf16, dxt)
+            else:
+                dx, dx_bf16, dw = ops().rmsnorm_bwd_add(dy2, s, weight, rstd, ds2, emit)
             dr = dx_bf16 if emit else (dx if ctx.r_dtype == dx.dtype else dx.to(ctx.r_dtype))
         return dx.view(ctx.shape), dr.view(ctx.shape), dw.to(weight.dtype), None, None
+
+
+def _want_transposed_grad(s: torch.Tensor) -> bool:
+    import os
+
+    H, M = s.shape[-1], s.numel() // s.shape[-1]
+    if os.environ.get("CS336_DYT", "1") == "0" or os.environ.get("CS336_DYT_FUSED", "1") == "0":
+        return False
+    rows = 16 if H * 36 <= 65536 else 8
+    return s.is_cuda and H % 8 == 0 and H <= 8192 and M % rows == 0
 
 
 def add_rmsnorm_ref(x, r, weight, eps=1e-5):

@@ -441,6 +441,35 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add(const at::Tensor&
   return {dx, dx2, dw};
 }
 
+// also returns the bf16 result transposed, (H, M) row-major, for the dW = dYᵀ·X GEMMs
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add_t(const at::Tensor& dy, const at::Tensor& x,
+                                                                             const at::Tensor& w, const at::Tensor& rstd,
+                                                                             const at::Tensor& dres, bool emit_bf16) {
+  check_cuda(dy, "dy");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes() && x.dim() == 2,
+              "cs336: rmsnorm_bwd_add_t shapes");
+  const int64_t M = x.size(0), H = x.size(1);
+  TORCH_CHECK(H % 8 == 0 && H <= 8192, "cs336: rmsnorm_bwd_add_t needs a hidden size divisible by 8, <= 8192");
+  TORCH_CHECK(M % cs336::rmsnorm_bwd_add_t_rows(H) == 0, "cs336: rmsnorm_bwd_add_t needs rows divisible by ",
+              cs336::rmsnorm_bwd_add_t_rows(H));
+  TORCH_CHECK(dres.is_contiguous() && dres.sizes() == x.sizes() && dres.scalar_type() == x.scalar_type(),
+              "cs336: rmsnorm_bwd_add_t dres must match x");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == H,
+              "cs336: rmsnorm_bwd_add_t weight must be fp32 (H)");
+  TORCH_CHECK(f32_or_bf16(dy) && f32_or_bf16(x), "cs336: rmsnorm_bwd_add_t dtypes must be fp32 or bf16");
+  c10::DeviceGuard g(x.device());
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dx2 = emit_bf16 ? at::empty_like(x, x.options().dtype(at::kBFloat16)) : at::empty({0}, x.options().dtype(at::kBFloat16));
+  at::Tensor dxt = at::empty({H, M}, x.options().dtype(at::kBFloat16));
+  if (M == 0) return {dx, dx2, dxt, at::zeros({H}, x.options().dtype(at::kFloat))};
+  at::Tensor dw = at::empty({H}, x.options().dtype(at::kFloat));
+  at::Tensor ws = at::empty({(int64_t)cs336::rmsnorm_bwd_add_t_workspace_rows(M, H), H}, x.options().dtype(at::kFloat));
+  cs336::rmsnorm_bwd_add_t(dy.data_ptr(), to_dtype(dy), x.data_ptr(), to_dtype(x), w.data_ptr<float>(),
+                           rstd.data_ptr<float>(), dres.data_ptr(), dx.data_ptr(), emit_bf16 ? dx2.data_ptr() : nullptr,
+                           dxt.data_ptr(), dw.data_ptr<float>(), ws.data_ptr<float>(), M, H, stream());
+  return {dx, dx2, dxt, dw};
+}
+
 // ------------------------------------------------------------------------------------------
 // RoPE
 // ------------------------------------------------------------------------------------------
@@ -746,6 +775,7 @@ TORCH_LIBRARY(cs336, m) {
   m.def("gemm_ok(Tensor a, Tensor b, bool trans_a, bool trans_b) -> bool", &gemm_ok);
   m.def("gemm_plan(int M, int N, int K, bool fp32_out) -> int[]", &gemm_plan);
   m.def("rmsnorm_bwd_add(Tensor dy, Tensor x, Tensor weight, Tensor rstd, Tensor dres, bool emit_bf16) -> (Tensor, Tensor, Tensor)");
+  m.def("rmsnorm_bwd_add_t(Tensor dy, Tensor x, Tensor weight, Tensor rstd, Tensor dres, bool emit_bf16) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, Tensor? pos, bool inverse) -> Tensor");
   m.def(
       "fa_bwd_into(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale, "
@@ -782,6 +812,7 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("gemm_out", &gemm_out);
   m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
   m.impl("rmsnorm_bwd_add", &rmsnorm_bwd_add);
+  m.impl("rmsnorm_bwd_add_t", &rmsnorm_bwd_add_t);
   m.impl("rope", &rope);
   m.impl("fa_bwd_into", &fa_bwd_into);
   m.impl("rope_into", &rope_into);

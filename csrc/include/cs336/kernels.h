@@ -20,6 +20,12 @@ int rmsnorm_bwd_workspace_rows(int64_t M, int64_t H);
 void add_rmsnorm_fwd(const void* x, DType xt, const void* r, DType rt, const float* w, void* y, DType yt, void* sum,
                      float* rstd, int64_t M, int64_t H, float eps, hipStream_t s);
 // dx = rmsnorm_bwd(dy) + dres (dtype xt, dres same dtype); dx_bf16 (optional) = bf16 copy of dx
+// rmsnorm_bwd_add that also writes the bf16 result transposed (dxt: H x M, ld M); M % rows == 0
+int rmsnorm_bwd_add_t_rows(int64_t H);
+int rmsnorm_bwd_add_t_workspace_rows(int64_t M, int64_t H);
+void rmsnorm_bwd_add_t(const void* dy, DType dyt, const void* x, DType xt, const float* w, const float* rstd,
+                       const void* dres, void* dx, void* dx_bf16, void* dxt, float* dw, float* workspace, int64_t M,
+                       int64_t H, hipStream_t s);
 void rmsnorm_bwd_add(const void* dy, DType dyt, const void* x, DType xt, const float* w, const float* rstd,
                      const void* dres, void* dx, void* dx_bf16, float* dw, float* workspace, int64_t M, int64_t H,
                      hipStream_t s);

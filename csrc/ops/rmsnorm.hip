@@ -170,6 +170,118 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const typename Elem<TD
   for (int i = threadIdx.x; i < H4; i += 256) reinterpret_cast<float4*>(wr)[i] = reinterpret_cast<float4*>(red)[i];
 }
 
+// Fused-residual backward that also writes the bf16 residual gradient TRANSPOSED, dxT[h][m]
+// (ld = M), for the narrow projections' weight-gradient GEMMs dW = dYᵀ·X (models/fused.py
+// `_dy_transposed`): their dY is this gradient, and a token-contiguous dYᵀ is the layout hipBLASLt
+// runs fastest. Workgroup = 16 consecutive rows (4 per wave); the bf16 rows are staged in LDS as
+// [h][16 rows] (pitch 18 halves: 2-4-way write conflicts instead of 16) and leave as one 32-B
+// piece per h, so two neighbouring workgroups fill a 64-B segment of a dxT row. Same math and dw
+// partials (one row per workgroup) as rmsnorm_bwd_kernel<..., ADD=true>. M % 16 == 0 (host).
+// R = 16 rows per workgroup while the staged tile fits 64 KB of LDS (H <= 1820), else 8.
+template <typename TDY, typename TX, int NV, int R>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_add_t_kernel(const typename Elem<TDY>::storage* __restrict__ dy,
+                                                                const typename Elem<TX>::storage* __restrict__ x,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ rstd,
+                                                                typename Elem<TX>::storage* __restrict__ dx,
+                                                                float* __restrict__ ws, int64_t M, int H,
+                                                                const typename Elem<TX>::storage* __restrict__ dres,
+                                                                bf16_t* __restrict__ dx2, bf16_t* __restrict__ dxt) {
+  constexpr int kTRows = R, kTPitch = R + 2;  // rows per workgroup, LDS halves per h
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // H * kTPitch halves, reused for dw
+  uint16_t* tile = reinterpret_cast<uint16_t*>(lds);
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int H4 = H >> 2;
+  const int64_t row0 = (int64_t)blockIdx.x * kTRows;
+  float4 wv[NV], dwp[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = lane + kWave * k;
+    wv[k] = i < H4 ? load4<float>(w + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    dwp[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float invH = 1.f / (float)H;
+  for (int rr = 0; rr < kTRows / 4; ++rr) {
+    const int lr = wave * (kTRows / 4) + rr;  // row within the workgroup
+    const int64_t row = row0 + lr;
+    const float r = rstd[row];
+    float4 xv[NV], gv[NV], dv[NV];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int i = lane + kWave * k;
+      if (i < H4) {
+        xv[k] = load4<TX>(x + row * H + 4 * i);
+        gv[k] = load4<TDY>(dy + row * H + 4 * i);
+        dv[k] = load4<TX>(dres + row * H + 4 * i);
+      } else {
+        xv[k] = gv[k] = dv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+      dot += wv[k].x * gv[k].x * xv[k].x + wv[k].y * gv[k].y * xv[k].y + wv[k].z * gv[k].z * xv[k].z +
+             wv[k].w * gv[k].w * xv[k].w;
+    dot = wave_sum(dot);
+    const float c = r * r * r * invH * dot;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int i = lane + kWave * k;
+      if (i < H4) {
+        float4 o;
+        o.x = r * wv[k].x * gv[k].x - c * xv[k].x + dv[k].x;
+        o.y = r * wv[k].y * gv[k].y - c * xv[k].y + dv[k].y;
+        o.z = r * wv[k].z * gv[k].z - c * xv[k].z + dv[k].z;
+        o.w = r * wv[k].w * gv[k].w - c * xv[k].w + dv[k].w;
+        store4<TX>(dx + row * H + 4 * i, o);
+        if (dx2) store4<BF16>(dx2 + row * H + 4 * i, o);
+        uint16_t* tp = tile + (4 * i) * kTPitch + lr;
+        tp[0] = __builtin_bit_cast(uint16_t, (__bf16)o.x);
+        tp[kTPitch] = __builtin_bit_cast(uint16_t, (__bf16)o.y);
+        tp[2 * kTPitch] = __builtin_bit_cast(uint16_t, (__bf16)o.z);
+        tp[3 * kTPitch] = __builtin_bit_cast(uint16_t, (__bf16)o.w);
+        dwp[k].x += gv[k].x * xv[k].x * r;
+        dwp[k].y += gv[k].y * xv[k].y * r;
+        dwp[k].z += gv[k].z * xv[k].z * r;
+        dwp[k].w += gv[k].w * xv[k].w * r;
+      }
+    }
+  }
+  __syncthreads();
+  // transposed store: thread -> (h, part): 8 rows of column h as one 16-B store
+  constexpr int PARTS = kTRows / 8;
+  for (int q = threadIdx.x; q < PARTS * H; q += 256) {
+    const int h = q / PARTS, half = q % PARTS;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(tile + h * kTPitch + 8 * half);
+    const uint4 v = make_uint4(src[0], src[1], src[2], src[3]);
+    *reinterpret_cast<uint4*>(dxt + (int64_t)h * M + row0 + 8 * half) = v;
+  }
+  __syncthreads();
+  // dw partials: fold the 4 waves through LDS (wave order: deterministic), one row per workgroup
+  float* red = reinterpret_cast<float*>(lds);
+  for (int wv_ = 0; wv_ < 4; ++wv_) {
+    if (wave == wv_) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int i = lane + kWave * k;
+        if (i < H4) {
+          float4* rp = reinterpret_cast<float4*>(red + 4 * i);
+          if (wv_ == 0) {
+            *rp = dwp[k];
+          } else {
+            float4 a = *rp;
+            a.x += dwp[k].x; a.y += dwp[k].y; a.z += dwp[k].z; a.w += dwp[k].w;
+            *rp = a;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* wr = ws + (int64_t)blockIdx.x * H;
+  for (int i = threadIdx.x; i < H4; i += 256) reinterpret_cast<float4*>(wr)[i] = reinterpret_cast<float4*>(red)[i];
+}
+
 // out[s][j] = sum over the partial rows p of split s of ws[p][j] (H % 4 == 0). Block = 64 float4
 // columns x 8 row slices; the slices are folded through LDS in a fixed order (deterministic).
 // grid (ceil(H/256), splits)
@@ -325,6 +437,47 @@ void rmsnorm_bwd_add(const void* dy, DType dyt, const void* x, DType xt, const f
                            (const typename Elem<TDY>::storage*)dy, (const typename Elem<TX>::storage*)x, w, rstd,
                            (typename Elem<TX>::storage*)dx, workspace, M, (int)H,
                            (const typename Elem<TX>::storage*)dres, (bf16_t*)dx_bf16);
+      });
+    });
+  });
+  float* split = workspace + (int64_t)nb * H;
+  const unsigned ct = (unsigned)((H / 4 + 63) / 64);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ct, kColSplits), dim3(512), 0, s, workspace, split, nb, (int)H);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ct, 1), dim3(512), 0, s, split, dw, kColSplits, (int)H);
+}
+
+}  // namespace cs336
+
+namespace cs336 {
+
+int rmsnorm_bwd_add_t_rows(int64_t H) { return H * 18 * 2 <= 65536 ? 16 : 8; }
+
+int rmsnorm_bwd_add_t_workspace_rows(int64_t M, int64_t H) {
+  return (int)(M / rmsnorm_bwd_add_t_rows(H)) + kColSplits;
+}
+
+void rmsnorm_bwd_add_t(const void* dy, DType dyt, const void* x, DType xt, const float* w, const float* rstd,
+                       const void* dres, void* dx, void* dx_bf16, void* dxt, float* dw, float* workspace, int64_t M,
+                       int64_t H, hipStream_t s) {
+  const int R = rmsnorm_bwd_add_t_rows(H);
+  const int nb = (int)(M / R);
+  const size_t tile = (size_t)H * (R + 2) * 2, red = (size_t)H * sizeof(float);
+  const size_t lds = tile > red ? tile : red;
+  dispatch_nv<0>((int)H, [&](auto nv) {
+    constexpr int NV = decltype(nv)::value;
+    dispatch_f32_bf16(dyt, [&](auto tdy) {
+      using TDY = decltype(tdy);
+      dispatch_f32_bf16(xt, [&](auto tx) {
+        using TX = decltype(tx);
+        auto go = [&](auto rr) {
+          constexpr int RR = decltype(rr)::value;
+          hipLaunchKernelGGL((rmsnorm_bwd_add_t_kernel<TDY, TX, NV, RR>), dim3(nb), dim3(256), lds, s,
+                             (const typename Elem<TDY>::storage*)dy, (const typename Elem<TX>::storage*)x, w, rstd,
+                             (typename Elem<TX>::storage*)dx, workspace, M, (int)H,
+                             (const typename Elem<TX>::storage*)dres, (bf16_t*)dx_bf16, (bf16_t*)dxt);
+        };
+        if (R == 16) go(std::integral_constant<int, 16>{});
+        else go(std::integral_constant<int, 8>{});
       });
     });
   });

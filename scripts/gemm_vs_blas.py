@@ -44,6 +44,9 @@ def main():
             # mixed: only X token-contiguous (saved transposed from the forward) / only dY
             "dw_xt": (lambda: torch.mm(dy.t(), xT.t(), out_dtype=torch.float32), dy, xT, True, True, torch.float32),
             "dw_dyt": (lambda: torch.mm(dyT, x, out_dtype=torch.float32), dyT, x, False, False, torch.float32),
+            # input gradient from a transposed dYᵀ (N_out, tokens): A operand M-contiguous
+            "dx_dyt": (lambda: dyT.t() @ w, dyT, w, True, False, torch.bfloat16),
+            "dx_dyt_wt": (lambda: dyT.t() @ wT.t(), dyT, wT, True, True, torch.bfloat16),
             # the model's layout: dY and X both token-major (A and B MN-major)
             "dw": (lambda: torch.mm(dy.t(), x, out_dtype=torch.float32), dy, x, True, False, torch.float32),
         }

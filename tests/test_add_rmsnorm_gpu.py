@@ -65,3 +65,46 @@ def test_model_fused_residual_matches_block_loop(monkeypatch):
     for n in g_loop:
         scale = g_loop[n].abs().max().item() + 1e-6
         torch.testing.assert_close(g_fused[n] / scale, g_loop[n] / scale, rtol=0, atol=3e-2, msg=n)
+
+
+@pytest.mark.parametrize("H", [64, 1600, 2560])
+@pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
+def test_rmsnorm_bwd_add_t_matches_row_major(H, xdt):
+    """The transposed-output residual backward (csrc/ops/rmsnorm.hip rmsnorm_bwd_add_t_kernel):
+    dx, dw and the bf16 copy equal rmsnorm_bwd_add's bitwise, and dxT is that copy transposed."""
+    assert ops.load_ext(), ops.load_error()
+    torch.manual_seed(0)
+    M = 16 * 37
+    s = torch.randn(M, H, device=DEV, dtype=xdt)
+    w = 1 + 0.1 * torch.randn(H, device=DEV)
+    rstd = torch.rsqrt(s.float().pow(2).mean(-1) + 1e-5)
+    dy = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
+    ds = torch.randn(M, H, device=DEV, dtype=xdt)
+    dx, dx2, dw = torch.ops.cs336.rmsnorm_bwd_add(dy, s, w, rstd, ds, True)
+    tx, tx2, txt, tw = torch.ops.cs336.rmsnorm_bwd_add_t(dy, s, w, rstd, ds, True)
+    assert torch.equal(dx, tx) and torch.equal(dx2, tx2)
+    torch.testing.assert_close(tw, dw, rtol=1e-5, atol=1e-4)  # partial-row grouping differs
+    assert txt.shape == (H, M) and torch.equal(txt, dx2.t())
+
+
+def test_model_grads_fused_dyt_vs_transpose(monkeypatch):
+    """Narrow-projection dW from the norm-written dYᵀ (offer/take) vs a separate transpose."""
+    grads = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CS336_DYT_FUSED", flag)
+        from cs336_systems.models import fused
+
+        fused._DYT_OFFERS.clear()
+        torch.manual_seed(0)
+        m = BasicsTransformerLM(vocab_size=512, context_length=128, d_model=256, num_layers=2, num_heads=4, d_ff=512,
+                                device=DEV)
+        x = torch.randint(0, 512, (4, 128), device=DEV, generator=torch.Generator(DEV).manual_seed(1))
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = ops.cross_entropy(m(x), x)
+        loss.backward()
+        if flag == "1":
+            assert not fused._DYT_OFFERS, "every offered dYᵀ should have been taken"
+        grads.append({n: p.grad.clone() for n, p in m.named_parameters()})
+    for n, g in grads[0].items():
+        # projection grads are bitwise equal; the norm gains sum their partial rows in other groups
+        torch.testing.assert_close(g, grads[1][n], rtol=1e-5, atol=1e-7, msg=n)
