@@ -358,6 +358,11 @@ def take_transposed_grad(g2: torch.Tensor) -> torch.Tensor | None:
     return gt if ok else None
 
 
+def _rope_out_in_fa() -> bool:
+    """Fuse the backward's inverse RoPE into the FA2 backward's dQ/dK store (CS336_FA_ROPE_OUT=0: off)."""
+    return os.environ.get("CS336_FA_ROPE_OUT", "1") != "0"
+
+
 def attn_out_transposed() -> bool:
     """The FA2 forward also writes Oᵀ for the output projection's weight gradient (CS336_OT=0: off)."""
     return os.environ.get("CS336_OT", "1") != "0"
@@ -572,8 +577,19 @@ class AttentionCore(torch.autograd.Function):
         if do.stride(-1) != 1:
             do = do.contiguous()
         hip = _hip()
-        hip.fa_bwd_into(do, qk[:, :H], qk[:, H:], v, o, lse, True, ctx.scale, dqk[:, :H], dqk[:, H:], dv)
-        hip.rope_into(dqk, cos, sin, pos, True, dqk)
+        rpos = pos
+        if rpos is not None and rpos.numel() != B * N:
+            rpos = rpos.expand(B, N)
+        if rpos is not None:
+            rpos = rpos.contiguous()
+        if _rope_out_in_fa() and N <= cos.shape[0]:
+            # dQ/dK rotated back inside the FA2 backward's store (q/k were rotated by the forward's
+            # RoPE pass): no separate inverse-RoPE pass over d(q|k)
+            hip.fa_bwd_into(do, qk[:, :H], qk[:, H:], v, o, lse, True, ctx.scale, dqk[:, :H], dqk[:, H:], dv,
+                            cos, sin, rpos, True)
+        else:
+            hip.fa_bwd_into(do, qk[:, :H], qk[:, H:], v, o, lse, True, ctx.scale, dqk[:, :H], dqk[:, H:], dv)
+            hip.rope_into(dqk, cos, sin, pos, True, dqk)
         return dqkv, None, None, None, None, None
 
 

@@ -101,7 +101,8 @@ def _l2(ts):
 
 
 @register_fake("cs336::fa_bwd_into")
-def _fa_bwd_into(do, q, k, v, o, lse, causal, scale, dq, dk, dv, rope_cos=None, rope_sin=None, rope_pos=None):
+def _fa_bwd_into(do, q, k, v, o, lse, causal, scale, dq, dk, dv, rope_cos=None, rope_sin=None, rope_pos=None,
+                 rope_out_only=False):
     return None
 
 

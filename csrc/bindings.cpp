@@ -161,7 +161,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_fwd_ot(const at::Tensor& q, co
 void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                 const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
                 const at::Tensor& dk, const at::Tensor& dv, const OptT& rope_cos, const OptT& rope_sin,
-                const OptT& rope_pos);
+                const OptT& rope_pos, bool rope_out_only = false);
 
 void check_bwd_inputs(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                       const at::Tensor& out, const at::Tensor& lse) {
@@ -193,7 +193,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_bwd(const at::Tensor& dout, co
 void fa_bwd_into(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                  const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
                  const at::Tensor& dk, const at::Tensor& dv, const OptT& rope_cos, const OptT& rope_sin,
-                 const OptT& rope_pos) {
+                 const OptT& rope_pos, bool rope_out_only) {
   check_bwd_inputs(dout, q, k, v, out, lse);
   check_bhnd(dq, "dq");
   check_bhnd(dk, "dk");
@@ -203,17 +203,18 @@ void fa_bwd_into(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& 
                   dv.scalar_type() == q.scalar_type(),
               "cs336: dtype mismatch");
   c10::DeviceGuard g(q.device());
-  fa_bwd_run(dout, q, k, v, out, lse, causal, scale, dq, dk, dv, rope_cos, rope_sin, rope_pos);
+  fa_bwd_run(dout, q, k, v, out, lse, causal, scale, dq, dk, dv, rope_cos, rope_sin, rope_pos, rope_out_only);
 }
 
 void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                 const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
                 const at::Tensor& dk, const at::Tensor& dv, const OptT& rope_cos, const OptT& rope_sin,
-                const OptT& rope_pos) {
+                const OptT& rope_pos, bool rope_out_only) {
   at::Tensor delta = at::empty({q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
   cs336::AttnBwdParams bp;
   fill_attn(bp.f, q, k, v, out, lse, causal, scale);
   set_rope(bp.f, q, k, rope_cos, rope_sin, rope_pos);
+  bp.f.rope_out_only = rope_out_only && bp.f.rope_cos != nullptr;
   bp.dout = dout.data_ptr();
   bp.do_sb = dout.stride(0); bp.do_sh = dout.stride(1); bp.do_sn = dout.stride(2);
   bp.dq = dq.data_ptr();
@@ -779,7 +780,8 @@ TORCH_LIBRARY(cs336, m) {
   m.def("rope(Tensor x, Tensor cos, Tensor sin, Tensor? pos, bool inverse) -> Tensor");
   m.def(
       "fa_bwd_into(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale, "
-      "Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None) -> ()");
+      "Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None, "
+      "bool rope_out_only=False) -> ()");
   m.def("rope_into(Tensor x, Tensor cos, Tensor sin, Tensor? pos, bool inverse, Tensor(a!) out) -> ()");
   m.def("swiglu_fused_fwd(Tensor y) -> Tensor");
   m.def("swiglu_fused_bwd(Tensor dh, Tensor y) -> Tensor");

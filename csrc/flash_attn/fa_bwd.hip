@@ -24,7 +24,7 @@ namespace fa {
 // ============================================================================================
 // dQ (+ delta) kernel
 // ============================================================================================
-template <typename T, int D, bool CAUSAL, bool ROPE, bool DMA>
+template <typename T, int D, bool CAUSAL, int ROPE, bool DMA>
 __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
   const AttnParams p = bp.f;  // by value: a reference would spill the kernarg struct to scratch
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   static_assert(BN * CPR % 256 == 0, "staging rounds must be whole");
   constexpr int NDT = DP / 32;
   constexpr bool PREFETCH = !(F32 && D == 128);
-  static_assert(!DMA || (!F32 && !ROPE), "LDS-DMA staging: 16-bit, no RoPE-on-load");
+  static_assert(!DMA || (!F32 && ROPE != 1), "LDS-DMA staging: 16-bit, no RoPE-on-load");
   constexpr int NS = DMA ? 3 : 2;  // K/V ring depth
 
   __shared__ __attribute__((aligned(1024))) char smem[NS * 2 * TILE];
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
     const int e = F32 ? (hh * (DP / 2) + 4 * i) : (16 * i + 8 * hh);
     if (valid_q && (DP == D || e < D)) {
       qf[i] = *reinterpret_cast<const uint4*>(Qp + (int64_t)qrow * p.q_sn + e);
-      if (ROPE) qf[i] = rope_chunk<T>(qf[i], rope, qpos, e, 1.f);
+      if (ROPE == 1) qf[i] = rope_chunk<T>(qf[i], rope, qpos, e, 1.f);
       dof[i] = *reinterpret_cast<const uint4*>(dOp + (int64_t)qrow * bp.do_sn + e);
       // delta partial over this lane's half of d
 #pragma unroll
@@ -101,14 +101,14 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   const int ntiles = (kv_end + BN - 1) / BN;
 
   uint4 kst[LPT], vst[LPT];
-  RopeCoef kst_rc[ROPE ? LPT : 1];  // rotation applied at LDS-write time (keeps the prefetch async)
+  RopeCoef kst_rc[ROPE == 1 ? LPT : 1];  // rotation applied at LDS-write time (keeps the prefetch async)
   auto gload = [&](int j) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i;
       const int r = c / CPR, ch = c % CPR;
       const int key = j * BN + r;
-      if (ROPE) kst_rc[i] = rope_coef<T>(rope, key < p.Nk ? (rpos ? rpos[key] : key) : 0, ch < CREAL ? ch * EPC : 0);
+      if (ROPE == 1) kst_rc[i] = rope_coef<T>(rope, key < p.Nk ? (rpos ? rpos[key] : key) : 0, ch < CREAL ? ch * EPC : 0);
       if (key < p.Nk && (CREAL == CPR || ch < CREAL)) {
         kst[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)key * p.k_sn + ch * EPC);
         vst[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)key * p.v_sn + ch * EPC);
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i;
       const int off = lds_off<RB>(c / CPR, c % CPR);
-      *reinterpret_cast<uint4*>(Ks + off) = ROPE ? rope_apply<T>(kst[i], kst_rc[i]) : kst[i];
+      *reinterpret_cast<uint4*>(Ks + off) = ROPE == 1 ? rope_apply<T>(kst[i], kst_rc[i]) : kst[i];
       *reinterpret_cast<uint4*>(Ks + TILE + off) = vst[i];
     }
   };
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
         if (DP != D && d >= D) continue;
         float v0 = dq[dt][4 * g] * sc, v1 = dq[dt][4 * g + 1] * sc, v2 = dq[dt][4 * g + 2] * sc,
               v3 = dq[dt][4 * g + 3] * sc;
-        if (ROPE) rope_inv4(v0, v1, v2, v3, rope, qpos, d);  // dQ w.r.t. the un-rotated q
+        if (ROPE != 0) rope_inv4(v0, v1, v2, v3, rope, qpos, d);  // dQ w.r.t. the un-rotated q
         store4<T>(row + d, make_float4(v0, v1, v2, v3));
       }
   }
@@ -286,7 +286,7 @@ constexpr int dkdv_min_waves() {
   return (D == 64 && !std::is_same<T, float>::value) ? 2 : 1;
 }
 
-template <typename T, int D, bool CAUSAL, bool ROPE, bool DMA>
+template <typename T, int D, bool CAUSAL, int ROPE, bool DMA>
 __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
   const AttnParams p = bp.f;  // by value: a reference would spill the kernarg struct to scratch
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
   static_assert(BQ * CPR % 256 == 0, "staging rounds must be whole");
   constexpr int NDT = DP / 32;
   constexpr bool PREFETCH = !(F32 && D == 128);
-  static_assert(!DMA || (!F32 && !ROPE), "LDS-DMA staging: 16-bit, no RoPE-on-load");
+  static_assert(!DMA || (!F32 && ROPE != 1), "LDS-DMA staging: 16-bit, no RoPE-on-load");
   // LDS-DMA slot: Q, dO images, then L and delta in 1 KB regions (one wave-instruction each)
   constexpr int BUFD = 2 * TILE + 2048;
   constexpr int NS = DMA ? (DP <= 96 ? 3 : 2) : (PREFETCH ? 2 : 1);
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
     const int e = F32 ? (hh * (DP / 2) + 4 * i) : (16 * i + 8 * hh);
     if (valid_k && (DP == D || e < D)) {
       kf[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)krow * p.k_sn + e);
-      if (ROPE) kf[i] = rope_chunk<T>(kf[i], rope, kpos, e, 1.f);
+      if (ROPE == 1) kf[i] = rope_chunk<T>(kf[i], rope, kpos, e, 1.f);
       vf[i] = *reinterpret_cast<const uint4*>(Vp + (int64_t)krow * p.v_sn + e);
     } else {
       kf[i] = vf[i] = make_uint4(0, 0, 0, 0);
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
   const int qt_end = (p.Nq + BQ - 1) / BQ;
 
   uint4 qst[LPT], dst[LPT];
-  RopeCoef qst_rc[ROPE ? LPT : 1];  // rotation applied at LDS-write time (keeps the prefetch async)
+  RopeCoef qst_rc[ROPE == 1 ? LPT : 1];  // rotation applied at LDS-write time (keeps the prefetch async)
   float lst = 0.f, dlt = 0.f;
   auto gload = [&](int it) {
     const int qbase = it * BQ;
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
       const int c = tid + 256 * i;
       const int r = c / CPR, ch = c % CPR;
       const int q = qbase + r;
-      if (ROPE) qst_rc[i] = rope_coef<T>(rope, q < p.Nq ? (rpos ? rpos[q] : q) : 0, ch < CREAL ? ch * EPC : 0);
+      if (ROPE == 1) qst_rc[i] = rope_coef<T>(rope, q < p.Nq ? (rpos ? rpos[q] : q) : 0, ch < CREAL ? ch * EPC : 0);
       if (q < p.Nq && (CREAL == CPR || ch < CREAL)) {
         qst[i] = *reinterpret_cast<const uint4*>(Qp + (int64_t)q * p.q_sn + ch * EPC);
         dst[i] = *reinterpret_cast<const uint4*>(dOp + (int64_t)q * bp.do_sn + ch * EPC);
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i;
       const int off = lds_off<RB>(c / CPR, c % CPR);
-      *reinterpret_cast<uint4*>(base + off) = ROPE ? rope_apply<T>(qst[i], qst_rc[i]) : qst[i];
+      *reinterpret_cast<uint4*>(base + off) = ROPE == 1 ? rope_apply<T>(qst[i], qst_rc[i]) : qst[i];
       *reinterpret_cast<uint4*>(base + TILE + off) = dst[i];
     }
     if (tid < BQ) {
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
         if (DP != D && d >= D) continue;
         float v0 = dk[dt][4 * g] * sc, v1 = dk[dt][4 * g + 1] * sc, v2 = dk[dt][4 * g + 2] * sc,
               v3 = dk[dt][4 * g + 3] * sc;
-        if (ROPE) rope_inv4(v0, v1, v2, v3, rope, kpos, d);  // dK w.r.t. the un-rotated k
+        if (ROPE != 0) rope_inv4(v0, v1, v2, v3, rope, kpos, d);  // dK w.r.t. the un-rotated k
         store4<T>(krow_dk + d, make_float4(v0, v1, v2, v3));
         store4<T>(krow_dv + d, make_float4(dv[dt][4 * g], dv[dt][4 * g + 1], dv[dt][4 * g + 2], dv[dt][4 * g + 3]));
       }
@@ -600,7 +600,7 @@ CS336_FA_BWD_DMA(F16, 80)
 CS336_FA_BWD_DMA(F16, 128)
 #undef CS336_FA_BWD_DMA
 
-template <typename T, int D, bool C, bool R, bool DMA>
+template <typename T, int D, bool C, int R, bool DMA>
 void launch_bwd_v(const AttnBwdParams& bp, hipStream_t s, dim3 gq, dim3 gk, dim3 block) {
   hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, C, R, DMA>), gq, block, 0, s, bp);
   hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, C, R, DMA>), gk, block, 0, s, bp);
@@ -608,10 +608,13 @@ void launch_bwd_v(const AttnBwdParams& bp, hipStream_t s, dim3 gq, dim3 gk, dim3
 
 template <typename T, int D, bool C>
 void launch_bwd_c(const AttnBwdParams& bp, hipStream_t s, dim3 gq, dim3 gk, dim3 block) {
-  if (bp.f.rope_cos != nullptr) {
-    launch_bwd_v<T, D, C, true, false>(bp, s, gq, gk, block);
+  if (bp.f.rope_cos != nullptr && bp.f.rope_out_only) {
+    // q/k were rotated by the forward's RoPE pass: only dQ/dK are rotated back, at their store
+    launch_bwd_v<T, D, C, 2, false>(bp, s, gq, gk, block);
+  } else if (bp.f.rope_cos != nullptr) {
+    launch_bwd_v<T, D, C, 1, false>(bp, s, gq, gk, block);
   } else if constexpr (!std::is_same<T, float>::value) {
-    if (bp.f.dma & 2) launch_bwd_v<T, D, C, false, true>(bp, s, gq, gk, block);
+    if (bp.f.dma & 2) launch_bwd_v<T, D, C, 0, true>(bp, s, gq, gk, block);
     else launch_bwd_v<T, D, C, false, false>(bp, s, gq, gk, block);
   } else {
     launch_bwd_v<T, D, C, false, false>(bp, s, gq, gk, block);

@@ -128,6 +128,9 @@ struct AttnParams {
   const float* rope_cos = nullptr;
   const float* rope_sin = nullptr;
   const int64_t* rope_pos = nullptr;
+  // backward only: q/k are ALREADY rotated (the model's separate RoPE pass); dq/dk are still
+  // returned w.r.t. the un-rotated inputs (inverse rotation fused into their store)
+  int rope_out_only = 0;
   // block dispatch order under the causal mask: 0 = per-(batch, head) interleaved, 1 = heaviest tile
   // level first within each XCD's heads (longest-processing-time order, see tile_order in fa_common.h)
   int order = 1;
