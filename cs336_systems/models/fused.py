@@ -364,8 +364,10 @@ def _rope_out_in_fa() -> bool:
 
 
 def attn_out_transposed() -> bool:
-    """The FA2 forward also writes Oᵀ for the output projection's weight gradient (CS336_OT=0: off)."""
-    return os.environ.get("CS336_OT", "1") != "0"
+    """The FA2 forward also writes Oᵀ for the output projection's weight gradient (CS336_OT=1: on).
+    Off by default: with dYᵀ for that GEMM the O-side layout gains less than the forward's extra
+    transposed store costs (same-box A/B on XL: 180.8 ms/step off vs 181.0 on)."""
+    return os.environ.get("CS336_OT", "0") == "1"
 
 
 def _mark_side_work() -> None:

@@ -89,6 +89,8 @@ def test_model_grads_rope_out_in_fa(monkeypatch):
             loss = ops.cross_entropy(m(x), x)
         loss.backward()
         grads.append({n: p.grad.clone() for n, p in m.named_parameters()})
+    worst = {}
     for n, g in grads[0].items():
-        scale = g.abs().max().item() + 1e-12
-        torch.testing.assert_close(g / scale, grads[1][n] / scale, rtol=0, atol=5e-3, msg=n)
+        worst[n] = float((g - grads[1][n]).norm() / grads[1][n].norm().clamp_min(1e-30))
+    # one bf16 rounding of dQ/dK (fused) vs two (separate pass): ~1e-3 relative on the grads
+    assert max(worst.values()) < 1e-2, sorted(worst.items(), key=lambda kv: -kv[1])[:4]
