@@ -48,8 +48,13 @@ def lt_gemm_enabled() -> bool:
     return _mode() in ("lt", "best")
 
 
-def _mode() -> str:
+def _mode(dw: bool = False) -> str:
+    """GEMM implementation mode; ``dw``: for the weight-gradient GEMMs, where ``CS336_GEMM_DW``
+    (if set) overrides ``CS336_GEMM`` — their fp32-output, long-K, small-output problems are the
+    ones hipBLASLt's default pick serves worst."""
     m = os.environ.get("CS336_GEMM", "blas").lower()
+    if dw:
+        m = os.environ.get("CS336_GEMM_DW", m).lower()
     return m if m in ("lt", "best", "hip") and ext_available() else "blas"
 
 
@@ -105,10 +110,10 @@ def _ok(a, b, ta, tb) -> bool:
     return a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and ops().gemm_ok(a, b, ta, tb)
 
 
-def _select(kind, a, b, out, blas, lt, cs336) -> str:
+def _select(kind, a, b, out, blas, lt, cs336, dw: bool = False) -> str:
     """Implementation for this call: ``lt``/``hip`` modes force theirs where it applies, ``best``
     times the applicable ones (``None`` = not applicable), ``blas`` is hipBLASLt's default."""
-    mode = _mode()
+    mode = _mode(dw)
     if mode == "lt" and lt is not None:
         return "lt"
     if mode == "hip" and cs336 is not None:
@@ -175,8 +180,8 @@ def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None =
     else:
         blas = lambda: torch.mm(dy.t(), xt.t(), out_dtype=torch.float32, out=out)  # noqa: E731
         lt = lambda: ops().lt_gemm_out(dy, xt, True, True, out)  # noqa: E731
-    use_lt = _mode() in ("lt", "best") and _lt_ok(dy, xt) and (out is None or out.stride(1) == 1)
-    r = (lt if use_lt and _select("tt32", dy, xt, out, blas, lt, None) == "lt" else blas)()
+    use_lt = _mode(True) in ("lt", "best") and _lt_ok(dy, xt) and (out is None or out.stride(1) == 1)
+    r = (lt if use_lt and _select("tt32", dy, xt, out, blas, lt, None, dw=True) == "lt" else blas)()
     return out if out is not None else r
 
 
@@ -189,7 +194,7 @@ def mm_dyt_fp32(dyt: torch.Tensor, x: torch.Tensor, x_is_t: bool, out: torch.Ten
         blas = lambda: torch.mm(dyt, b, out_dtype=torch.float32)  # noqa: E731
     else:
         blas = lambda: torch.mm(dyt, b, out_dtype=torch.float32, out=out)  # noqa: E731
-    if _mode() == "blas" or not dyt.is_cuda:
+    if _mode(True) == "blas" or not dyt.is_cuda:
         r = blas()
         return out if out is not None else r
     lt_ok = _lt_ok(dyt, x) and (out is None or out.stride(1) == 1)
@@ -199,7 +204,7 @@ def mm_dyt_fp32(dyt: torch.Tensor, x: torch.Tensor, x_is_t: bool, out: torch.Ten
     else:
         lt = (lambda: ops().lt_gemm_out(dyt, x, False, x_is_t, out)) if lt_ok else None
         cs = (lambda: ops().gemm_out(dyt, x, False, x_is_t, out, False, 0, 0, 0)) if _ok(dyt, x, False, x_is_t) else None
-    r = {"blas": blas, "lt": lt, "cs336": cs}[_select("dyt32" + ("t" if x_is_t else "n"), dyt, x, out, blas, lt, cs)]()
+    r = {"blas": blas, "lt": lt, "cs336": cs}[_select("dyt32" + ("t" if x_is_t else "n"), dyt, x, out, blas, lt, cs, dw=True)]()
     return out if out is not None else r
 
 
@@ -216,7 +221,7 @@ def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = Non
                 return torch.mm(dy.t(), x).float()
     else:
         blas = lambda: torch.mm(dy.t(), x, out_dtype=torch.float32, out=out)  # noqa: E731
-    if _mode() == "blas" or not dy.is_cuda:
+    if _mode(True) == "blas" or not dy.is_cuda:
         r = blas()
         return out if out is not None else r
     lt_ok = _lt_ok(dy, x) and (out is None or out.stride(1) == 1)
@@ -226,5 +231,5 @@ def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = Non
     else:
         lt = (lambda: ops().lt_gemm_out(dy, x, True, False, out)) if lt_ok else None
         cs = (lambda: ops().gemm_out(dy, x, True, False, out, False, 0, 0, 0)) if _ok(dy, x, True, False) else None
-    r = {"blas": blas, "lt": lt, "cs336": cs}[_select("tn32", dy, x, out, blas, lt, cs)]()
+    r = {"blas": blas, "lt": lt, "cs336": cs}[_select("tn32", dy, x, out, blas, lt, cs, dw=True)]()
     return out if out is not None else r
