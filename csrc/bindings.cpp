@@ -87,11 +87,13 @@ void fill_attn(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, c
   // forward +12-24 % without the causal mask and +3 % at d 128 causal, -2 % at d 64 causal; the
   // backward kernels lose 2-7 % (their time is not in the tile loads). CS336_FA_DMA: unset = that
   // choice, 0 = never, 1 = every forward, 2 = forward and backward.
-  static const int dma_env = [] {
+  const int dma_env = [] {  // read per call (cheap next to a launch): tests switch it in-process
     const char* e = std::getenv("CS336_FA_DMA");
     return e && *e ? std::atoi(e) : -1;
   }();
+  // 4: the forward's pipelined variant (separate K/V rings, next S^T inside this tile's softmax)
   if (dma_env < 0) p.dma = (!causal || p.D >= 128) ? 1 : 0;
+  else if (dma_env == 4) p.dma = 1 | 4;
   else p.dma = dma_env == 0 ? 0 : (dma_env == 1 ? 1 : 3);
 }
 

@@ -21,16 +21,21 @@ namespace fa {
 
 // 16-bit variants ask for two workgroups per CU (<= 256 VGPRs): without the hint the LDS-DMA variant
 // at d 128 took 260 registers, ran one workgroup per CU and lost 37 % (causal, N 4096)
-template <typename T, int D>
+// The pipelined variant (DMA 2) holds two S^T tiles: one workgroup per CU except at d 64 without
+// the causal mask, where two still fit 256 VGPRs (measured spills otherwise: 72-148 B/lane).
+template <typename T, int D, bool CAUSAL = false, int DMA = 0>
 constexpr int fwd_min_waves() {
 #ifdef CS336_FA_FWD_WAVES64
   if (D <= 64 && !std::is_same<T, float>::value) return CS336_FA_FWD_WAVES64;
 #endif
+  if (DMA == 2) return (D <= 64 && !CAUSAL) ? 2 : 1;
   return std::is_same<T, float>::value ? 1 : 2;
 }
 
-template <typename T, int D, bool CAUSAL, bool ROPE, bool DMA>
-__global__ __launch_bounds__(256, (fwd_min_waves<T, D>())) void fa_fwd_kernel(const AttnParams p) {
+// DMA: 0 = VGPR staging, 1 = LDS-DMA ring of K|V tiles, 2 = LDS-DMA into separate K and V rings
+// with the next tile's S^T MFMAs issued inside the current tile's softmax (software pipeline)
+template <typename T, int D, bool CAUSAL, bool ROPE, int DMA>
+__global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_fwd_kernel(const AttnParams p) {
   typedef typename Elem<T>::storage S;
   constexpr bool F32 = std::is_same<T, float>::value;
   constexpr int ES = sizeof(S);
@@ -47,6 +52,7 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D>())) void fa_fwd_kernel(co
   constexpr bool PREFETCH = !(F32 && D == 128);
   static_assert(!DMA || (!F32 && !ROPE), "LDS-DMA staging: 16-bit, no RoPE-on-load");
   // LDS-DMA ring depth: 3 K/V stages (two tiles in flight) up to 96-wide rows, 2 at d 128
+  // (DMA 2: NS slots in each of the K and V rings, the same bytes)
   constexpr int NS = DMA ? (DP <= 96 ? 3 : 2) : 2;
 
   __shared__ __attribute__((aligned(1024))) char smem[NS * 2 * TILE];
@@ -123,100 +129,169 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D>())) void fa_fwd_kernel(co
   for (int i = 0; i < NDT; ++i) o[i] = zero16();
   const float c2 = p.scale * kLog2e;
 
-  // one K/V tile's work: S^T, mask, online softmax, O^T += V^T P^T (Ks: the tile's K image, V after it)
-  auto tile = [&](int j, const char* Ks) {
-    const int kt0 = j * BN;
-    const bool active = !CAUSAL || kt0 <= qw0 + 31;
-    if (active) {
-      const char* Vs = Ks + TILE;
-      f32x16 s[2];
-      // ---- S^T = K Q^T ----
+  // one K/V tile's work, in two parts so the pipelined loop can put the NEXT tile's S^T MFMAs
+  // between this tile's softmax VALU work: s_tile = S^T = K Q^T (Ks: the tile's K image);
+  // finish = mask, online softmax, O^T += V^T P^T (Vs: the tile's V image), with `mid` issued after
+  // the rescale branch, in the same basic block as the exp2 loop and the PV MFMAs
+  auto active = [&](int j) { return !CAUSAL || j * BN <= qw0 + 31; };
+  auto s_tile = [&](const char* Ks, f32x16 (&s)[2]) {
+    // ---- S^T = K Q^T ----
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        s[t] = zero16();
-        if constexpr (F32) {
+    for (int t = 0; t < 2; ++t) {
+      s[t] = zero16();
+      if constexpr (F32) {
 #pragma unroll
-          for (int i = 0; i < DP / 8; ++i) {
-            const float4 kv = lds_f4<RB>(Ks, 32 * t + l32, hh * (DP / 2) + 4 * i);
-            const float4 qv = __builtin_bit_cast(float4, qf[i]);
-            s[t] = mma_f32(kv.x, qv.x, s[t]);
-            s[t] = mma_f32(kv.y, qv.y, s[t]);
-            s[t] = mma_f32(kv.z, qv.z, s[t]);
-            s[t] = mma_f32(kv.w, qv.w, s[t]);
-          }
-        } else {
-#pragma unroll
-          for (int ks = 0; ks < DP / 16; ++ks)
-            s[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Ks, 32 * t, ks, lane), as_frag<T>(qf[ks]), s[t]);
+        for (int i = 0; i < DP / 8; ++i) {
+          const float4 kv = lds_f4<RB>(Ks, 32 * t + l32, hh * (DP / 2) + 4 * i);
+          const float4 qv = __builtin_bit_cast(float4, qf[i]);
+          s[t] = mma_f32(kv.x, qv.x, s[t]);
+          s[t] = mma_f32(kv.y, qv.y, s[t]);
+          s[t] = mma_f32(kv.z, qv.z, s[t]);
+          s[t] = mma_f32(kv.w, qv.w, s[t]);
         }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < DP / 16; ++ks)
+          s[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Ks, 32 * t, ks, lane), as_frag<T>(qf[ks]), s[t]);
       }
-      // ---- mask (bounds / causal diagonal) ----
-      const bool need_mask = (kt0 + BN > p.Nk) || (CAUSAL && kt0 + BN - 1 > qw0);
-      if (need_mask) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kt0 + 32 * t + acc_row(r, hh);
-            if (key >= p.Nk || (CAUSAL && key > qrow)) s[t][r] = -INFINITY;
-          }
-      }
-      // ---- online softmax (query on the lane), deferred rescale (T13) ----
-      float mx = s[0][0];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[t][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mt = mx * c2;
-      if (__ballot(mt > m + kRescaleThr) != 0) {  // wave-uniform
-        const float m_new = fmaxf(m, mt);
-        const float alpha = fexp2(m - m_new);
-        l *= alpha;
-        m = m_new;
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-      }
-      float rs = 0.f;
+    }
+  };
+  auto finish = [&](int j, const char* Vs, f32x16 (&s)[2], auto&& mid) {
+    const int kt0 = j * BN;
+    // ---- mask (bounds / causal diagonal) ----
+    const bool need_mask = (kt0 + BN > p.Nk) || (CAUSAL && kt0 + BN - 1 > qw0);
+    if (need_mask) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float pv = fexp2(fmaf(s[t][r], c2, -m));
-          s[t][r] = pv;
-          rs += pv;
+          const int key = kt0 + 32 * t + acc_row(r, hh);
+          if (key >= p.Nk || (CAUSAL && key > qrow)) s[t][r] = -INFINITY;
         }
-      l += rs;
-      // ---- O^T += V^T P^T ----
-      if constexpr (F32) {
+    }
+    // ---- online softmax (query on the lane), deferred rescale (T13) ----
+    float mx = s[0][0];
 #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[t][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mt = mx * c2;
+    if (__ballot(mt > m + kRescaleThr) != 0) {  // wave-uniform
+      const float m_new = fmaxf(m, mt);
+      const float alpha = fexp2(m - m_new);
+      l *= alpha;
+      m = m_new;
 #pragma unroll
-            for (int r = 0; r < 16; ++r)
-              o[dt] = mma_f32(lds_f1<RB>(Vs, 32 * t + acc_row(r, hh), dt * 32 + l32), s[t][r], o[dt]);
-      } else {
-        typename Mma16<T>::frag pf[2][2];
+      for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          pf[t][0] = pack_acc<T>(s[t], 0);
-          pf[t][1] = pack_acc<T>(s[t], 1);
-        }
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+    }
+    mid();
+    float rs = 0.f;
 #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
-              o[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Vs, 32 * t, s2, dt, lane), pf[t][s2], o[dt]);
+      for (int r = 0; r < 16; ++r) {
+        const float pv = fexp2(fmaf(s[t][r], c2, -m));
+        s[t][r] = pv;
+        rs += pv;
       }
+    l += rs;
+    // ---- O^T += V^T P^T ----
+    if constexpr (F32) {
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            o[dt] = mma_f32(lds_f1<RB>(Vs, 32 * t + acc_row(r, hh), dt * 32 + l32), s[t][r], o[dt]);
+    } else {
+      typename Mma16<T>::frag pf[2][2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        pf[t][0] = pack_acc<T>(s[t], 0);
+        pf[t][1] = pack_acc<T>(s[t], 1);
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+            o[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Vs, 32 * t, s2, dt, lane), pf[t][s2], o[dt]);
+    }
+  };
+  auto tile = [&](int j, const char* Ks) {
+    if (active(j)) {
+      f32x16 s[2];
+      s_tile(Ks, s);
+      finish(j, Ks + TILE, s, [] {});
     }
   };
 
-  if constexpr (DMA) {
+  if constexpr (DMA == 2) {
+    // Separate K and V rings of NS slots each (K ring at smem, V ring after it). Iteration j needs
+    // K(j+1) (for the next S^T) and V(j) (for this PV); it then refills the slots freed by the
+    // previous iteration: V(j+NS-1) and K(j+NS). Groups past the last tile are still issued (an
+    // empty buffer range: the loads return zeros) so every wait below is one static count: after
+    // K(j+1) and V(j), exactly 2*NS-4 younger groups of this wave are in flight.
+    using Dma = TileDma<BN, RB, CREAL, ES>;
+    constexpr int PW = Dma::PER_WAVE;
+    Dma kd, vd;
+    kd.init(wave, lane, p.k_sn);
+    vd.init(wave, lane, p.v_sn);
+    char* Kr = smem;
+    char* Vr = smem + NS * TILE;
+    if (D != DP || p.Nk % BN != 0) {
+      lds_zero(smem, NS * 2 * TILE);
+      __syncthreads();
+    }
+    auto issue_k = [&](int j) {
+      const int rows = min(BN, p.Nk - j * BN);
+      kd.issue(Kp + (int64_t)j * BN * p.k_sn, rows, p.k_sn, Kr + (j % NS) * TILE, wave);
+    };
+    auto issue_v = [&](int j) {
+      const int rows = min(BN, p.Nk - j * BN);
+      vd.issue(Vp + (int64_t)j * BN * p.v_sn, rows, p.v_sn, Vr + (j % NS) * TILE, wave);
+    };
+    // prologue: K(0), V(0), K(1), V(1), ..., K(NS-2), V(NS-2), K(NS-1)
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t) {
+      issue_k(t);
+      issue_v(t);
+    }
+    issue_k(NS - 1);
+    wait_vmcnt<(2 * NS - 2) * PW>();  // K(0) landed
+    __syncthreads();
+    f32x16 sa[2], sb[2];
+    if (active(0)) s_tile(Kr, sa);
+    // one iteration: publish K(j+1), V(j); refill; finish tile j with S^T(j+1) inside its softmax
+    auto body = [&](int j, f32x16 (&cur)[2], f32x16 (&nxt)[2]) {
+      wait_vmcnt<(2 * NS - 4) * PW>();
+      __syncthreads();
+      issue_v(j + NS - 1);
+      issue_k(j + NS);
+      if (active(j)) finish(j, Vr + (j % NS) * TILE, cur, [&] { s_tile(Kr + ((j + 1) % NS) * TILE, nxt); });
+    };
+    auto last = [&](int j, f32x16 (&cur)[2]) {
+      wait_vmcnt<0>();  // V(j) (and the trailing empty groups)
+      __syncthreads();
+      if (active(j)) finish(j, Vr + (j % NS) * TILE, cur, [] {});
+    };
+    int j = 0;
+    for (; j + 2 < ntiles; j += 2) {  // unrolled by two: sa/sb swap roles with static names
+      body(j, sa, sb);
+      body(j + 1, sb, sa);
+    }
+    if (j + 1 < ntiles) {
+      body(j, sa, sb);
+      last(j + 1, sb);
+    } else if (j < ntiles) {
+      last(j, sa);
+    }
+  } else if constexpr (DMA) {
     using Dma = TileDma<BN, RB, CREAL, ES>;
     Dma kd, vd;
     kd.init(wave, lane, p.k_sn);
@@ -320,9 +395,11 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D>())) void fa_fwd_kernel(co
 
 // Explicit instantiation of the LDS-DMA variants: hipcc (ROCm 7.2) referenced some of them from the
 // launch chain below without emitting their host stubs (undefined __device_stub__ at load time).
-#define CS336_FA_FWD_DMA(T, D)                                                     \
-  template __global__ void fa_fwd_kernel<T, D, false, false, true>(const AttnParams); \
-  template __global__ void fa_fwd_kernel<T, D, true, false, true>(const AttnParams);
+#define CS336_FA_FWD_DMA(T, D)                                                  \
+  template __global__ void fa_fwd_kernel<T, D, false, false, 1>(const AttnParams); \
+  template __global__ void fa_fwd_kernel<T, D, true, false, 1>(const AttnParams);  \
+  template __global__ void fa_fwd_kernel<T, D, false, false, 2>(const AttnParams); \
+  template __global__ void fa_fwd_kernel<T, D, true, false, 2>(const AttnParams);
 CS336_FA_FWD_DMA(BF16, 32)
 CS336_FA_FWD_DMA(BF16, 64)
 CS336_FA_FWD_DMA(BF16, 80)
@@ -336,12 +413,13 @@ CS336_FA_FWD_DMA(F16, 128)
 template <typename T, int D, bool C>
 void launch_fwd_c(const AttnParams& p, hipStream_t s, dim3 grid, dim3 block) {
   if (p.rope_cos != nullptr) {
-    hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, true, false>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, true, 0>), grid, block, 0, s, p);
   } else if constexpr (!std::is_same<T, float>::value) {
-    if (p.dma & 1) hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, true>), grid, block, 0, s, p);
-    else hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, false>), grid, block, 0, s, p);
+    if (p.dma & 4) hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, 2>), grid, block, 0, s, p);
+    else if (p.dma & 1) hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, 1>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, 0>), grid, block, 0, s, p);
   } else {
-    hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, false>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((fa_fwd_kernel<T, D, C, false, 0>), grid, block, 0, s, p);
   }
 }
 

@@ -96,3 +96,13 @@ def test_flash_seq4096(D, causal):
 def test_flash_leaderboard_shape_subset():
     """(16, 16384, 64) causal bf16 as (B=16, H=1): one head per XCD range end is checked."""
     _run(16, 1, 16384, 64, True, [(0, 0), (7, 0), (15, 0)])
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("D", [64, 128])
+def test_flash_seq4096_pipelined_forward(monkeypatch, D, causal):
+    """CS336_FA_DMA=4: the software-pipelined forward (separate K/V LDS-DMA rings, next tile's S^T
+    inside this tile's softmax) at the benchmarked shapes, plus a ragged length (partial last tile)."""
+    monkeypatch.setenv("CS336_FA_DMA", "4")
+    _run(2, 4, 4096, D, causal, [(0, 0), (1, 3)])
+    _run(1, 2, 1000, D, causal, [(0, 0), (0, 1)])
