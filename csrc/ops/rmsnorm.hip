@@ -10,6 +10,8 @@
 // Backward: each wave walks a strided set of rows, producing dx per row and accumulating its dw
 // partial in registers; partials (one per wave) go to a workspace that a column-tiled kernel
 // reduces (deterministic, no float atomics).
+#include <cstdlib>
+
 #include "cs336/kernels.h"
 
 namespace cs336 {
@@ -450,7 +452,11 @@ void rmsnorm_bwd_add(const void* dy, DType dyt, const void* x, DType xt, const f
 
 namespace cs336 {
 
-int rmsnorm_bwd_add_t_rows(int64_t H) { return H * 18 * 2 <= 65536 ? 16 : 8; }
+int rmsnorm_bwd_add_t_rows(int64_t H) {
+  const char* e = std::getenv("CS336_DYT_ROWS");  // A/B: 8 or 16 rows per workgroup
+  if (e && std::atoi(e) == 8) return 8;
+  return H * 18 * 2 <= 65536 ? 16 : 8;
+}
 
 int rmsnorm_bwd_add_t_workspace_rows(int64_t M, int64_t H) {
   return (int)(M / rmsnorm_bwd_add_t_rows(H)) + kColSplits;
