@@ -29,6 +29,9 @@ constexpr int fwd_min_waves() {
   if (D <= 64 && !std::is_same<T, float>::value) return CS336_FA_FWD_WAVES64;
 #endif
   if (DMA == 2) return (D <= 64 && !CAUSAL) ? 2 : 1;
+  // d <= 64 causal with VGPR staging: three workgroups per CU (168 VGPRs, no spill): +11-12 % at
+  // N 512 and 4096 (profiles/r2_fa_fwd_waves.md); the other d-64 variants would spill at 168
+  if (D <= 64 && CAUSAL && DMA == 0 && !std::is_same<T, float>::value) return 3;
   return std::is_same<T, float>::value ? 1 : 2;
 }
 
