@@ -99,9 +99,16 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
         obj = _obj_for(src)
         if force or _stale(src, obj, hdr_mtime):
             with open(src) as fh:
-                # pure-MFMA kernels (GEMM) keep accumulators in AGPRs: no VALU touches them in the loop
-                agpr = "cs336-build: agpr-accumulators" in fh.read(4096)
+                head = fh.read(4096)
+            # pure-MFMA kernels (GEMM) keep accumulators in AGPRs: no VALU touches them in the loop
+            agpr = "cs336-build: agpr-accumulators" in head
             flags = kflags if not agpr else [f for f in kflags if f not in VGPR_FORM]
+            # MFMA loops with f32 elementwise work between the chains: keep that work scalar. The SLP
+            # vectorizer packs adjacent f32 multiplies into v_pk_mul_f32, which needs register-pair
+            # moves and re-aligned bf16 packing (FA2 backward dK/dV loop: 251 -> 211 VALU per 32 MFMA)
+            # and is slower than two single ops beside MFMAs (MI355X_MICROARCH.md, filler prices)
+            if "cs336-build: no-slp" in head:
+                flags = flags + ["-fno-slp-vectorize"]
             jobs_list.append([hipcc, *flags, "-c", src, "-o", obj])
     for src in host:
         obj = _obj_for(src)

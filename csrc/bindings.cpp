@@ -212,7 +212,7 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
                 const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
                 const at::Tensor& dk, const at::Tensor& dv, const OptT& rope_cos, const OptT& rope_sin,
                 const OptT& rope_pos, bool rope_out_only) {
-  at::Tensor delta = at::empty({q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
+  at::Tensor delta = at::empty({2, q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
   cs336::AttnBwdParams bp;
   fill_attn(bp.f, q, k, v, out, lse, causal, scale);
   set_rope(bp.f, q, k, rope_cos, rope_sin, rope_pos);
@@ -226,6 +226,7 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
   bp.dk_sb = dk.stride(0); bp.dk_sh = dk.stride(1); bp.dk_sn = dk.stride(2);
   bp.dv_sb = dv.stride(0); bp.dv_sh = dv.stride(1); bp.dv_sn = dv.stride(2);
   bp.delta = delta.data_ptr<float>();
+  bp.lrow = bp.delta + q.size(0) * q.size(1) * q.size(2);
   cs336::flash_attn_bwd(bp, to_dtype(q), stream());
 }
 

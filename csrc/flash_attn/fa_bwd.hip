@@ -1,4 +1,5 @@
 // FlashAttention-2 backward for MI355X (gfx950 / CDNA4).
+// cs336-build: no-slp
 //
 // Parity: reference cs336_systems/flash_attention.py:270-289 (torch.compile of a recompute
 // backward that materializes the full N x N S/P/dP/dS — O(N^2) memory) and the handout's
@@ -95,7 +96,11 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   }
   delta += __shfl_xor(delta, 32, 64);
   const float lse2 = valid_q ? p.lse[row_lin] * kLog2e : INFINITY;
-  if (valid_q && hh == 0) bp.delta[row_lin] = delta;
+  // row constants of the dK/dV kernel, pre-transformed so they load straight into its accumulators
+  if (valid_q && hh == 0) {
+    bp.delta[row_lin] = -delta;
+    bp.lrow[row_lin] = -lse2;
+  }
 
   const int kv_end = CAUSAL ? min(p.Nk, q0 + BM) : p.Nk;
   const int ntiles = (kv_end + BN - 1) / BN;
@@ -286,6 +291,12 @@ constexpr int dkdv_min_waves() {
   return (D == 64 && !std::is_same<T, float>::value) ? 2 : 1;
 }
 
+// Staging position of query row r (0..63) of a tile so that lane-half h of 32-row group t finds
+// its 16 accumulator rows (acc_row(reg, h) = (reg & 3) + 8 (reg >> 2) + 4h) at 32t + 16h + reg.
+__device__ __forceinline__ int row_perm(int r) {
+  return (r & ~31) | (((r >> 2) & 1) << 4) | (((r >> 3) & 3) << 2) | (r & 3);
+}
+
 template <typename T, int D, bool CAUSAL, int ROPE, bool DMA>
 __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
@@ -296,7 +307,9 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
   constexpr int RB = DP * ES, CPR = RB / 16, EPC = 16 / ES, CREAL = D * ES / 16;
   // -delta as the dP accumulators' initial value (+1-2 % at d64/d128); at the padded d80 the extra
   // live row constants cost more than the saved subtraction (-17 %), so it keeps the explicit form
-  constexpr bool DINIT = DP == D;
+  // (16-bit only: with the fp32 MFMA chains the accumulator-initialising loads crash hipcc's
+  // AGPR-copy rewrite in the d128 instances)
+  constexpr bool DINIT = DP == D && !F32;
   // 64-query tiles; at D=128 (one workgroup per CU anyway) part of the state lives in AGPRs
   // rather than halving the tile: 1153 -> 1046 us at N=4096 (fp32 keeps 32-query tiles)
   constexpr int BK = 128, BQ = (D == 128 && std::is_same<T, float>::value) ? 32 : 64;
@@ -330,7 +343,8 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
   const S* Kp = (const S*)p.k + b * p.k_sb + h * p.k_sh;
   const S* Vp = (const S*)p.v + b * p.v_sb + h * p.v_sh;
   const S* dOp = (const S*)bp.dout + b * bp.do_sb + h * bp.do_sh;
-  const float* Lp = p.lse + ((int64_t)b * p.H + h) * p.Nq;
+  // per-query row constants written by the dQ kernel: -lse log2(e) and -delta (dP accumulator start)
+  const float* Lp = bp.lrow + ((int64_t)b * p.H + h) * p.Nq;
   const float* Dp = bp.delta + ((int64_t)b * p.H + h) * p.Nq;
   S* dKp = (S*)bp.dk + b * bp.dk_sb + h * bp.dk_sh;
   S* dVp = (S*)bp.dv + b * bp.dv_sb + h * bp.dv_sh;
@@ -377,7 +391,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
     }
     if (tid < BQ) {
       const int q = qbase + tid;
-      lst = q < p.Nq ? Lp[q] * kLog2e : INFINITY;
+      lst = q < p.Nq ? Lp[q] : -INFINITY;  // P = exp2(c2 S - lse log2 e) = 0 past Nq
       dlt = q < p.Nq ? Dp[q] : 0.f;
     }
   };
@@ -391,8 +405,9 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
       *reinterpret_cast<uint4*>(base + TILE + off) = dst[i];
     }
     if (tid < BQ) {
-      reinterpret_cast<float*>(base + 2 * TILE)[tid] = lst;
-      reinterpret_cast<float*>(base + 2 * TILE + BQ * 4)[tid] = dlt;
+      const int pos = DINIT ? row_perm(tid) : tid;
+      reinterpret_cast<float*>(base + 2 * TILE)[pos] = lst;
+      reinterpret_cast<float*>(base + 2 * TILE + BQ * 4)[pos] = dlt;
     }
   };
 
@@ -404,117 +419,135 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
   }
   const float c2 = p.scale * kLog2e;
 
-  // one query tile: S, dP, P, dS, dV^T += dO^T P, dK^T += Q^T dS (Qs: the slot's Q image, dO after it)
-  auto tile = [&](int it, const char* Qs) {
+  // one query tile: S, dP, P, dS, dV^T += dO^T P, dK^T += Q^T dS (Qs: the slot's Q image, dO after it).
+  // The row constant -delta starts the dP accumulators (DINIT; loaded from the staged rows straight
+  // into them) and -lse log2(e) is pre-scaled, so P = exp2(fma(S, c2, L')) and dS = P dP' need no
+  // further VALU op; the
+  // causal/Nq mask is a separate instantiation taken only on diagonal (or ragged) tiles, so the bulk
+  // of the tiles carries no compare/select per element.
+  auto tile = [&](int it, const char* Qs, auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;
     const int qt0 = it * BQ;
-    const bool active = !CAUSAL || (qt0 + BQ - 1 >= kw0);
-    if (active) {
-      const char* dOs = Qs + TILE;
-      // L and delta rows: pre-scaled L2 after the VGPR staging, raw natural-log L after LDS-DMA
-      const float* Ls = reinterpret_cast<const float*>(Qs + 2 * TILE);
-      const float* Ds = DMA ? Ls + 256 : Ls + BQ;
-      const float lscale = DMA ? kLog2e : 1.f;
-      f32x16 s[NT], dp[NT];
+    if (CAUSAL && qt0 + BQ - 1 < kw0) return;  // whole tile above this wave's keys
+    const char* dOs = Qs + TILE;
+    const float* Ls = reinterpret_cast<const float*>(Qs + 2 * TILE);
+    const float* Ds = DMA ? Ls + 256 : Ls + BQ;
+    f32x16 s[NT], dp[NT];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        s[t] = zero16();
-        // dP accumulators start at -delta[q] (row constants per register): dS = P dP' afterwards
-        if constexpr (DINIT) {
+    for (int t = 0; t < NT; ++t) {
+      if constexpr (DINIT) {
+        // the rows are staged in accumulator order (row_perm): one 64-B read lands in the
+        // registers the dP chain accumulates into
+#ifndef CS336_DINIT_F4
+        dp[t] = *reinterpret_cast<const f32x16*>(Ds + 32 * t + 16 * hh);
+#else
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const float4 D4 = *reinterpret_cast<const float4*>(Ds + 32 * t + 8 * g + 4 * hh);
-            dp[t][4 * g] = -D4.x;
-            dp[t][4 * g + 1] = -D4.y;
-            dp[t][4 * g + 2] = -D4.z;
-            dp[t][4 * g + 3] = -D4.w;
-          }
-        } else {
-          dp[t] = zero16();
+        for (int g = 0; g < 4; ++g) {
+          const float4 D4 = *reinterpret_cast<const float4*>(Ds + 32 * t + 16 * hh + 4 * g);
+          dp[t][4 * g] = D4.x; dp[t][4 * g + 1] = D4.y; dp[t][4 * g + 2] = D4.z; dp[t][4 * g + 3] = D4.w;
         }
-        if constexpr (F32) {
+#endif
+      } else {
+        dp[t] = zero16();
+      }
+      s[t] = zero16();
+      if constexpr (F32) {
 #pragma unroll
-          for (int i = 0; i < DP / 8; ++i) {
-            const float4 qv = lds_f4<RB>(Qs, 32 * t + l32, hh * (DP / 2) + 4 * i);
-            const float4 gv = lds_f4<RB>(dOs, 32 * t + l32, hh * (DP / 2) + 4 * i);
-            const float4 kv = __builtin_bit_cast(float4, kf[i]);
-            const float4 vv = __builtin_bit_cast(float4, vf[i]);
-            s[t] = mma_f32(qv.x, kv.x, s[t]);
-            s[t] = mma_f32(qv.y, kv.y, s[t]);
-            s[t] = mma_f32(qv.z, kv.z, s[t]);
-            s[t] = mma_f32(qv.w, kv.w, s[t]);
-            dp[t] = mma_f32(gv.x, vv.x, dp[t]);
-            dp[t] = mma_f32(gv.y, vv.y, dp[t]);
-            dp[t] = mma_f32(gv.z, vv.z, dp[t]);
-            dp[t] = mma_f32(gv.w, vv.w, dp[t]);
-          }
-        } else {
+        for (int i = 0; i < DP / 8; ++i) {
+          const float4 qv = lds_f4<RB>(Qs, 32 * t + l32, hh * (DP / 2) + 4 * i);
+          const float4 gv = lds_f4<RB>(dOs, 32 * t + l32, hh * (DP / 2) + 4 * i);
+          const float4 kv = __builtin_bit_cast(float4, kf[i]);
+          const float4 vv = __builtin_bit_cast(float4, vf[i]);
+          s[t] = mma_f32(qv.x, kv.x, s[t]);
+          s[t] = mma_f32(qv.y, kv.y, s[t]);
+          s[t] = mma_f32(qv.z, kv.z, s[t]);
+          s[t] = mma_f32(qv.w, kv.w, s[t]);
+          dp[t] = mma_f32(gv.x, vv.x, dp[t]);
+          dp[t] = mma_f32(gv.y, vv.y, dp[t]);
+          dp[t] = mma_f32(gv.z, vv.z, dp[t]);
+          dp[t] = mma_f32(gv.w, vv.w, dp[t]);
+        }
+      } else {
 #pragma unroll
-          for (int ks = 0; ks < DP / 16; ++ks) {
-            s[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Qs, 32 * t, ks, lane), as_frag<T>(kf[ks]), s[t]);
-            dp[t] = Mma16<T>::mma(lds_row_frag<T, RB>(dOs, 32 * t, ks, lane), as_frag<T>(vf[ks]), dp[t]);
-          }
+        for (int ks = 0; ks < DP / 16; ++ks) {
+          s[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Qs, 32 * t, ks, lane), as_frag<T>(kf[ks]), s[t]);
+          dp[t] = Mma16<T>::mma(lds_row_frag<T, RB>(dOs, 32 * t, ks, lane), as_frag<T>(vf[ks]), dp[t]);
         }
       }
-      // P = exp2(S*c - L2[q]); dS = P (dP - delta[q]); rows (q) are in registers
-      const bool need_mask = (CAUSAL && (qt0 < kw0 + 31)) || (DMA && qt0 + BQ > p.Nq);
+    }
+    // P = exp2(c2 S - lse log2 e); dS = P (dP - delta); rows (q) are in registers
+    {
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int qr = 32 * t + 8 * g + 4 * hh;
-          const float4 L4 = *reinterpret_cast<const float4*>(Ls + qr);
+          const int qr = 32 * t + 8 * g + 4 * hh;  // query row of register 4g (+u)
+          const int lpos = DINIT ? 32 * t + 16 * hh + 4 * g : qr;  // its staging position
+          const float4 L4 = *reinterpret_cast<const float4*>(Ls + lpos);
           const float Lv[4] = {L4.x, L4.y, L4.z, L4.w};
-          float4 D4 = make_float4(0.f, 0.f, 0.f, 0.f);
-          if constexpr (!DINIT) D4 = *reinterpret_cast<const float4*>(Ds + qr);
-          const float Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+          float Dv[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (!DINIT) {
+            const float4 D4 = *reinterpret_cast<const float4*>(Ds + qr);
+            Dv[0] = D4.x; Dv[1] = D4.y; Dv[2] = D4.z; Dv[3] = D4.w;
+          }
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int r = 4 * g + u;
-            float pv = fexp2(fmaf(s[t][r], c2, -Lv[u] * lscale));
-            if (need_mask && ((CAUSAL && krow > qt0 + qr + u) || (DMA && qt0 + qr + u >= p.Nq))) pv = 0.f;
+            float pv = fexp2(fmaf(s[t][r], c2, Lv[u]));
+            if constexpr (MASK) {
+              if ((CAUSAL && krow > qt0 + qr + u) || (DMA && qt0 + qr + u >= p.Nq)) pv = 0.f;
+            }
             s[t][r] = pv;
-            dp[t][r] = DINIT ? pv * dp[t][r] : pv * (dp[t][r] - Dv[u]);
+            dp[t][r] = DINIT ? pv * dp[t][r] : pv * (dp[t][r] + Dv[u]);
           }
         }
-      if constexpr (F32) {
+    }
+    if constexpr (F32) {
 #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
+      for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-          for (int t = 0; t < NT; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int qr = 32 * t + acc_row(r, hh);
-              dv[dt] = mma_f32(lds_f1<RB>(dOs, qr, dt * 32 + l32), s[t][r], dv[dt]);
-              dk[dt] = mma_f32(lds_f1<RB>(Qs, qr, dt * 32 + l32), dp[t][r], dk[dt]);
-            }
-      } else {
-        typename Mma16<T>::frag pf[NT][2], sf[NT][2];
+          for (int r = 0; r < 16; ++r) {
+            const int qr = 32 * t + acc_row(r, hh);
+            dv[dt] = mma_f32(lds_f1<RB>(dOs, qr, dt * 32 + l32), s[t][r], dv[dt]);
+            dk[dt] = mma_f32(lds_f1<RB>(Qs, qr, dt * 32 + l32), dp[t][r], dk[dt]);
+          }
+    } else {
+      typename Mma16<T>::frag pf[NT][2], sf[NT][2];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          pf[t][0] = pack_acc<T>(s[t], 0);
-          pf[t][1] = pack_acc<T>(s[t], 1);
-          sf[t][0] = pack_acc<T>(dp[t], 0);
-          sf[t][1] = pack_acc<T>(dp[t], 1);
-        }
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-          for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-              dv[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(dOs, 32 * t, s2, dt, lane), pf[t][s2], dv[dt]);
-              dk[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Qs, 32 * t, s2, dt, lane), sf[t][s2], dk[dt]);
-            }
+      for (int t = 0; t < NT; ++t) {
+        pf[t][0] = pack_acc<T>(s[t], 0);
+        pf[t][1] = pack_acc<T>(s[t], 1);
+        sf[t][0] = pack_acc<T>(dp[t], 0);
+        sf[t][1] = pack_acc<T>(dp[t], 1);
       }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            dv[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(dOs, 32 * t, s2, dt, lane), pf[t][s2], dv[dt]);
+            dk[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Qs, 32 * t, s2, dt, lane), sf[t][s2], dk[dt]);
+          }
     }
   };
 
+  // Tiles that need the causal mask for some wave (the diagonal ones, qt0 < k0 + BK - 1) and, with
+  // LDS-DMA staging, a ragged last tile (rows past Nq are not -inf-padded there) run a masked
+  // instantiation of the tile; the bulk runs without the per-element compare/select.
+  const int mask_end = CAUSAL ? min(qt_end, (k0 + BK - 2) / BQ + 1) : qt_begin;
+  const int ragged = (DMA && p.Nq % BQ != 0) ? 1 : 0;
   if constexpr (DMA) {
     using Dma = TileDma<BQ, RB, CREAL, ES>;
     Dma qd, dd;
     qd.init(wave, lane, p.q_sn);
     dd.init(wave, lane, bp.do_sn);
-    const uint32_t row_off = lane < 16 ? 16u * lane : 0x80000000u;  // L / delta: 64 floats = 16 lanes
+    // L / delta: 64 floats = 16 lanes of 16 B; LDS chunk c holds source rows 4 row_perm^-1 chunk
+    // (accumulator order, see row_perm) when the tile reads them as whole accumulators
+    const int lsrc = DINIT ? 8 * (lane >> 3) + 2 * (lane & 3) + ((lane >> 2) & 1) : lane;
+    const uint32_t row_off = lane < 16 ? 16u * lsrc : 0x80000000u;
     if (D != DP || p.Nq % BQ != 0) {  // some slots are read out of range: start from zeros
       lds_zero(smem, NS * SLOT);
       __syncthreads();
@@ -534,34 +567,43 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
 #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
       if (qt_begin + t < qt_end) issue(qt_begin + t);
-    for (int it = qt_begin; it < qt_end; ++it) {
-      if (NS == 3 && it + 1 < qt_end) wait_vmcnt<PER_TILE>();
-      else wait_vmcnt<0>();
-      __syncthreads();
-      if (it + NS - 1 < qt_end) issue(it + NS - 1);
-      tile(it, smem + ((it - qt_begin) % NS) * SLOT);
-    }
+    auto run = [&](int lo, int hi, auto mask_tag) {
+      for (int it = lo; it < hi; ++it) {
+        if (NS == 3 && it + 1 < qt_end) wait_vmcnt<PER_TILE>();
+        else wait_vmcnt<0>();
+        __syncthreads();
+        if (it + NS - 1 < qt_end) issue(it + NS - 1);
+        tile(it, smem + ((it - qt_begin) % NS) * SLOT, mask_tag);
+      }
+    };
+    if constexpr (CAUSAL) run(qt_begin, mask_end, std::true_type{});
+    run(mask_end, qt_end - ragged, std::false_type{});
+    run(max(mask_end, qt_end - ragged), qt_end, std::true_type{});
   } else {
     if (qt_begin < qt_end) {
       gload(qt_begin);
       swrite(0);
     }
     __syncthreads();
-    for (int it = qt_begin; it < qt_end; ++it) {
-      const int buf = PREFETCH ? ((it - qt_begin) & 1) : 0;
-      if (PREFETCH && it + 1 < qt_end) gload(it + 1);
-      tile(it, smem + buf * BUF);
-      if (it + 1 < qt_end) {
-        if (PREFETCH) {
-          swrite(buf ^ 1);
-        } else {
-          __syncthreads();
-          gload(it + 1);
-          swrite(0);
+    auto run = [&](int lo, int hi, auto mask_tag) {
+      for (int it = lo; it < hi; ++it) {
+        const int buf = PREFETCH ? ((it - qt_begin) & 1) : 0;
+        if (PREFETCH && it + 1 < qt_end) gload(it + 1);
+        tile(it, smem + buf * BUF, mask_tag);
+        if (it + 1 < qt_end) {
+          if (PREFETCH) {
+            swrite(buf ^ 1);
+          } else {
+            __syncthreads();
+            gload(it + 1);
+            swrite(0);
+          }
         }
+        __syncthreads();
       }
-      __syncthreads();
-    }
+    };
+    if constexpr (CAUSAL) run(qt_begin, mask_end, std::true_type{});
+    run(mask_end, qt_end, std::false_type{});
   }
 
   if (valid_k) {

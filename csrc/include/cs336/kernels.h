@@ -154,7 +154,10 @@ struct AttnBwdParams {
   int64_t dq_sb, dq_sh, dq_sn;
   int64_t dk_sb, dk_sh, dk_sn;
   int64_t dv_sb, dv_sh, dv_sn;
-  float* delta;  // (B, H, Nq) workspace
+  // (B, H, Nq) workspaces written by the dQ kernel for the dK/dV kernel: the row constants
+  // -delta (delta = rowsum(dO * O)) and -lse / scale, loaded as the initial dP and S accumulators
+  float* delta;
+  float* lrow;
 };
 
 void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s);
