@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
             o[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Vs, 32 * t, s2, dt, lane), pf[t][s2], o[dt]);
     }
   };
-  auto tile = [&](int j, const char* Ks) {
+  auto tile = [&](int j, const char* Ks) __attribute__((always_inline)) {
     if (active(j)) {
       f32x16 s[2];
       s_tile(Ks, s);
@@ -312,15 +312,33 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
 #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
       if (t < ntiles) issue(t);
-    for (int j = 0; j < ntiles; ++j) {
+    auto step = [&](int j, auto slot) __attribute__((always_inline)) {
       // this wave's pieces of tile j have landed once only the younger tiles' DMAs are in flight;
       // the barrier then publishes every wave's pieces and retires all reads of tile j-1's slot
       if (NS == 3 && j + 1 < ntiles) wait_vmcnt<2 * Dma::PER_WAVE>();
       else wait_vmcnt<0>();
       __syncthreads();
       if (j + NS - 1 < ntiles) issue(j + NS - 1);
-      tile(j, smem + (j % NS) * 2 * TILE);
+      const int B = slot;  // integral_constant (unrolled loop) or runtime slot
+      tile(j, smem + B * 2 * TILE);
+    };
+    int j = 0;
+#ifndef CS336_FA_FWD_NO_UNROLL
+    // unrolled by the ring depth with compile-time slots: the slots' LDS addresses become immediates
+    if constexpr (NS == 3) {
+      for (; j + 2 < ntiles; j += 3) {
+        step(j, std::integral_constant<int, 0>{});
+        step(j + 1, std::integral_constant<int, 1>{});
+        step(j + 2, std::integral_constant<int, 2>{});
+      }
+    } else if constexpr (NS == 2) {
+      for (; j + 1 < ntiles; j += 2) {
+        step(j, std::integral_constant<int, 0>{});
+        step(j + 1, std::integral_constant<int, 1>{});
+      }
     }
+#endif
+    for (; j < ntiles; ++j) step(j, j % NS);
   } else {
     if (ntiles > 0) {
       gload(0);
