@@ -83,8 +83,9 @@ void fill_attn(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, c
   // heads whose K+V fit one XCD's 4 MB L2 form one level-major group (tile_order, fa_common.h)
   const int64_t kv_head = 2 * (int64_t)p.Nk * p.D * (int64_t)q.element_size();
   p.lpt_group = (int)std::max<int64_t>(1, std::min<int64_t>(1 << 20, (int64_t(4) << 20) / std::max<int64_t>(kv_head, 1)));
-  // LDS-DMA staging (fa_common.h TileDma), measured per kernel at N 4096 (scripts/fa_ab.py):
-  // forward +12-24 % without the causal mask and +3 % at d 128 causal, -2 % at d 64 causal; the
+  // LDS-DMA staging (fa_common.h TileDma), measured per kernel (scripts/fa_ab.py): with the DMA
+  // loop unrolled by its ring depth the forward gains everywhere except causal at short N (d64 causal
+  // N 4096 +7.5 %, d80 causal N 1024 +5 %, d64 causal N 512 -1.3 %, profiles/r2_fa_bwd_valu.md); the
   // backward kernels lose 2-7 % (their time is not in the tile loads). CS336_FA_DMA: unset = that
   // choice, 0 = never, 1 = every forward, 2 = forward and backward.
   const int dma_env = [] {  // read per call (cheap next to a launch): tests switch it in-process
@@ -92,7 +93,7 @@ void fill_attn(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, c
     return e && *e ? std::atoi(e) : -1;
   }();
   // 4: the forward's pipelined variant (separate K/V rings, next S^T inside this tile's softmax)
-  if (dma_env < 0) p.dma = (!causal || p.D >= 128) ? 1 : 0;
+  if (dma_env < 0) p.dma = (!causal || p.D >= 128 || p.Nk >= 1024) ? 1 : 0;
   else if (dma_env == 4) p.dma = 1 | 4;
   else p.dma = dma_env == 0 ? 0 : (dma_env == 1 ? 1 : 3);
 }
