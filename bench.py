@@ -46,9 +46,11 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="xl")
     ap.add_argument("--ctx", type=int, default=512)
-    # 24 x 512 = 12288 tokens per GPU: the best hipBLASLt shapes for this model on MI355X (measured
-    # 16 -> 53.3k, 24 -> 59.2k, 32 -> 55.7k tok/s on 1 GPU; scripts/gemm_bench.py explains why)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("CS336_BENCH_BATCH", 24)), help="per-GPU batch")
+    # 48 x 512 = 24576 tokens per GPU. Per-GPU batch sweep of the XL step on 1x MI355X
+    # (scripts/batch_sweep.sh, profiles/r2_batch_sweep.md): multiples of 24 run the best hipBLASLt
+    # shapes (24 -> 68.5k, 48 -> 69.4-69.7k, 72 -> 68.9k tok/s; 32/40/64/96 -> 65.2-65.8k); 48 also
+    # doubles the backward that hides each step's 8 GB of gradient all-reduce under DDP, at 116 GiB.
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("CS336_BENCH_BATCH", 48)), help="per-GPU batch")
     ap.add_argument("--vocab", type=int, default=10000)
     ap.add_argument(
         "--ddp",
