@@ -81,6 +81,14 @@ def parse(argv=None):
         # the GPU 97 % busy, so the HBM-bound update only competes with the GEMMs (profiles/README.md)
         help="run the AdamW update during backward on a side stream (auto: on GPU when clip == 0 and not sharded)",
     )
+    ap.add_argument(
+        "--gemm",
+        default=os.environ.get("CS336_GEMM", "best"),
+        choices=["blas", "lt", "best", "hip"],
+        # same-box A/B at batch 48 (profiles/r2_batch_sweep.md): blas 354.1/355.0 ms/step, lt 340.6/342.9,
+        # best 331.4/332.2 (the autotuned / cs336 picks win on W1|W3 dX, the o-projection and lm_head)
+        help="projection GEMM selection (cs336_systems/ops/gemm.py); sets CS336_GEMM",
+    )
     ap.add_argument("--graphs", action="store_true", help="1 GPU: replay forward+backward from one captured HIP graph")
     ap.add_argument(
         "--tunableop",
@@ -168,6 +176,7 @@ def main(argv=None):
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     rank = int(os.environ.get("RANK", "0"))
 
+    os.environ["CS336_GEMM"] = args.gemm  # read per call by cs336_systems.ops.gemm
     from cs336_systems import ops
     from cs336_systems.data import synthetic_batch
     from cs336_systems.models import build_model, get_model_config, param_count, train_flops_per_token
@@ -287,7 +296,10 @@ def main(argv=None):
         if world > 1:
             dist.barrier()
 
-    for i in range(args.warmup):
+    # lt/best GEMM modes time their candidates the first time each problem shape is seen: with
+    # --warmup 0 one untimed step still runs so that selection never lands inside the timed region
+    n_warm = max(args.warmup, 1) if device.type == "cuda" and args.gemm in ("lt", "best") else args.warmup
+    for i in range(n_warm):
         loss = step(i)
         sync()
         log(f"warmup {i}: loss {loss.item():.4f}")
