@@ -236,13 +236,23 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
 #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
       if (t < ntiles) issue(t);
-    for (int j = 0; j < ntiles; ++j) {
+    auto dstep = [&](int j, auto slot) __attribute__((always_inline)) {
       if (NS == 3 && j + 1 < ntiles) wait_vmcnt<2 * Dma::PER_WAVE>();
       else wait_vmcnt<0>();
       __syncthreads();
       if (j + NS - 1 < ntiles) issue(j + NS - 1);
-      tile(j, smem + (j % NS) * 2 * TILE);
+      const int B = slot;  // integral_constant (unrolled loop) or runtime slot
+      tile(j, smem + B * 2 * TILE);
+    };
+    int j = 0;
+    if constexpr (UNROLL2 && NS == 3) {  // unrolled by the ring depth: compile-time slots
+      for (; j + 2 < ntiles; j += 3) {
+        dstep(j, std::integral_constant<int, 0>{});
+        dstep(j + 1, std::integral_constant<int, 1>{});
+        dstep(j + 2, std::integral_constant<int, 2>{});
+      }
     }
+    for (; j < ntiles; ++j) dstep(j, j % NS);
   } else {
     if (ntiles > 0) {
       gload(0);
@@ -582,14 +592,28 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
 #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
       if (qt_begin + t < qt_end) issue(qt_begin + t);
+    auto dstep = [&](int it, auto slot, auto mask_tag) __attribute__((always_inline)) {
+      if (NS == 3 && it + 1 < qt_end) wait_vmcnt<PER_TILE>();
+      else wait_vmcnt<0>();
+      __syncthreads();
+      if (it + NS - 1 < qt_end) issue(it + NS - 1);
+      const int B = slot;  // integral_constant (unrolled loop) or runtime slot
+      tile(it, smem + B * SLOT, mask_tag);
+    };
     auto run = [&](int lo, int hi, auto mask_tag) __attribute__((always_inline)) {
-      for (int it = lo; it < hi; ++it) {
-        if (NS == 3 && it + 1 < qt_end) wait_vmcnt<PER_TILE>();
-        else wait_vmcnt<0>();
-        __syncthreads();
-        if (it + NS - 1 < qt_end) issue(it + NS - 1);
-        tile(it, smem + ((it - qt_begin) % NS) * SLOT, mask_tag);
+      int it = lo;
+      if constexpr (UNROLL2 && NS == 3) {  // unrolled by the ring depth: compile-time slots
+        while (it < hi && (it - qt_begin) % 3 != 0) {
+          dstep(it, (it - qt_begin) % 3, mask_tag);
+          ++it;
+        }
+        for (; it + 2 < hi; it += 3) {
+          dstep(it, std::integral_constant<int, 0>{}, mask_tag);
+          dstep(it + 1, std::integral_constant<int, 1>{}, mask_tag);
+          dstep(it + 2, std::integral_constant<int, 2>{}, mask_tag);
+        }
       }
+      for (; it < hi; ++it) dstep(it, (it - qt_begin) % NS, mask_tag);
     };
     if constexpr (CAUSAL) run(qt_begin, mask_end, std::true_type{});
     run(mask_end, qt_end - ragged, std::false_type{});
