@@ -93,11 +93,10 @@ void fill_attn(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, c
     return e && *e ? std::atoi(e) : -1;
   }();
   // 4: the forward's pipelined variant (separate K/V rings, next S^T inside this tile's softmax)
-  // backward (bit 2): with the dQ / dK-dV DMA loops unrolled by their ring depth (d <= 64) LDS-DMA
-  // staging wins at Nk >= 1024 for d 64 (+5 %) and for non-causal d 128 (+10 %); it loses 2 % at the
-  // XL step's N 512 and at causal d 128 (profiles/r2_fa_bwd_valu.md)
-  if (dma_env < 0)
-    p.dma = ((!causal || p.D >= 128 || p.Nk >= 1024) ? 1 : 0) | ((p.Nk >= 1024 && (p.D <= 64 || !causal)) ? 2 : 0);
+  // backward (bit 2): with the dQ / dK-dV DMA loops unrolled by their ring depth LDS-DMA staging
+  // wins at Nk >= 1024 (d 64 +5 %, d 128 +5-10 %, d 80 even); it loses 2 % at the XL step's N 512
+  // (profiles/r2_fa_bwd_valu.md)
+  if (dma_env < 0) p.dma = ((!causal || p.D >= 128 || p.Nk >= 1024) ? 1 : 0) | (p.Nk >= 1024 ? 2 : 0);
   else if (dma_env == 4) p.dma = 1 | 4;
   else p.dma = dma_env == 0 ? 0 : (dma_env == 1 ? 1 : 3);
 }

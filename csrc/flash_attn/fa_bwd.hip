@@ -50,6 +50,9 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   // VGPR-staged loop unrolled by two (compile-time slots, immediate LDS offsets): 5.3 instead of 7.6
   // VALU per MFMA at d64 (+6 % backward); at d80/d128 the extra live registers cost more (-10-16 %)
   constexpr bool UNROLL2 = DP <= 64;
+  // LDS-DMA loop unrolled by its ring depth at every d (no staging registers to add): d128 causal
+  // backward 492 -> 531 TF (profiles/r2_fa_bwd_valu.md)
+  constexpr bool DUNROLL = true;
 
   __shared__ __attribute__((aligned(1024))) char smem[NS * 2 * TILE];
 
@@ -245,7 +248,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
       tile(j, smem + B * 2 * TILE);
     };
     int j = 0;
-    if constexpr (UNROLL2 && NS == 3) {  // unrolled by the ring depth: compile-time slots
+    if constexpr (DUNROLL && NS == 3) {  // unrolled by the ring depth: compile-time slots
       for (; j + 2 < ntiles; j += 3) {
         dstep(j, std::integral_constant<int, 0>{});
         dstep(j + 1, std::integral_constant<int, 1>{});
@@ -350,6 +353,9 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
   constexpr int NS = DMA ? (DP <= 96 ? 3 : 2) : (PREFETCH ? 2 : 1);
   constexpr int SLOT = DMA ? BUFD : BUF;
   constexpr bool UNROLL2 = DP <= 64;  // see fa_bwd_dq_kernel
+  // LDS-DMA loop unrolled by its ring depth at every d (no staging registers to add): d128 causal
+  // backward 492 -> 531 TF (profiles/r2_fa_bwd_valu.md)
+  constexpr bool DUNROLL = true;
 
   __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT];
 
@@ -602,7 +608,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
     };
     auto run = [&](int lo, int hi, auto mask_tag) __attribute__((always_inline)) {
       int it = lo;
-      if constexpr (UNROLL2 && NS == 3) {  // unrolled by the ring depth: compile-time slots
+      if constexpr (DUNROLL && NS == 3) {  // unrolled by the ring depth: compile-time slots
         while (it < hi && (it - qt_begin) % 3 != 0) {
           dstep(it, (it - qt_begin) % 3, mask_tag);
           ++it;
@@ -611,6 +617,15 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
           dstep(it, std::integral_constant<int, 0>{}, mask_tag);
           dstep(it + 1, std::integral_constant<int, 1>{}, mask_tag);
           dstep(it + 2, std::integral_constant<int, 2>{}, mask_tag);
+        }
+      } else if constexpr (DUNROLL && NS == 2) {
+        if (it < hi && ((it - qt_begin) & 1)) {
+          dstep(it, 1, mask_tag);
+          ++it;
+        }
+        for (; it + 1 < hi; it += 2) {
+          dstep(it, std::integral_constant<int, 0>{}, mask_tag);
+          dstep(it + 1, std::integral_constant<int, 1>{}, mask_tag);
         }
       }
       for (; it < hi; ++it) dstep(it, (it - qt_begin) % NS, mask_tag);
