@@ -318,12 +318,6 @@ constexpr int dkdv_min_waves() {
   return (D == 64 && !std::is_same<T, float>::value) ? 2 : 1;
 }
 
-// Staging position of query row r (0..63) of a tile so that lane-half h of 32-row group t finds
-// its 16 accumulator rows (acc_row(reg, h) = (reg & 3) + 8 (reg >> 2) + 4h) at 32t + 16h + reg.
-__device__ __forceinline__ int row_perm(int r) {
-  return (r & ~31) | (((r >> 2) & 1) << 4) | (((r >> 3) & 3) << 2) | (r & 3);
-}
-
 template <typename T, int D, bool CAUSAL, int ROPE, bool DMA>
 __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
@@ -577,7 +571,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
     dd.init(wave, lane, bp.do_sn);
     // L / delta: 64 floats = 16 lanes of 16 B; LDS chunk c holds source rows 4 row_perm^-1 chunk
     // (accumulator order, see row_perm) when the tile reads them as whole accumulators
-    const int lsrc = DINIT ? 8 * (lane >> 3) + 2 * (lane & 3) + ((lane >> 2) & 1) : lane;
+    const int lsrc = DINIT ? row_perm_src_chunk(lane) : lane;
     const uint32_t row_off = lane < 16 ? 16u * lsrc : 0x80000000u;
     if (D != DP || p.Nq % BQ != 0) {  // some slots are read out of range: start from zeros
       lds_zero(smem, NS * SLOT);

@@ -305,7 +305,17 @@ __device__ __forceinline__ void lds_zero(char* p, int bytes) {
 }
 
 // key (or row) index held by accumulator register `reg` of lane-half h in a 32x32 tile
-__device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+__host__ __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// Staging position of query row r (0..63) of a backward tile so that lane-half h of 32-row group t
+// finds its 16 accumulator rows (acc_row(reg, h)) at 32t + 16h + reg: one 64-B read per lane loads
+// a row-constant accumulator (fa_bwd.hip dK/dV kernel).
+__host__ __device__ __forceinline__ int row_perm(int r) {
+  return (r & ~31) | (((r >> 2) & 1) << 4) | (((r >> 3) & 3) << 2) | (r & 3);
+}
+// LDS-DMA form of the same staging: 16 lanes move 16 B each; lane c (LDS chunk c = positions
+// 4c..4c+3) reads source chunk row_perm_src_chunk(c) (rows 4 src .. 4 src + 3)
+__host__ __device__ __forceinline__ int row_perm_src_chunk(int c) { return 8 * (c >> 3) + 2 * (c & 3) + ((c >> 2) & 1); }
 
 // Bijective XCD-aware remap of a 1-D block id: blocks that share a (batch, head) — and hence the
 // same K/V (or Q/dO) stream — become contiguous in the remapped order, i.e. share one XCD's L2

@@ -123,7 +123,27 @@ static void check_names() {
   CHECK(macro_tile_area("Cijk_noMT") == 0 && macro_tile_area("_MTx") == 0, "no MT");
 }
 
+// the dK/dV kernel's row-constant staging: row_perm is a bijection on each 64-row tile that puts
+// accumulator register reg of lane-half h (32-row group t) at 32t + 16h + reg, and the LDS-DMA
+// source chunks land the same rows in the same places
+static void check_row_perm() {
+  std::set<int> seen;
+  for (int r = 0; r < 64; ++r) {
+    CHECK(row_perm(r) >= 0 && row_perm(r) < 64, "row_perm(%d) out of range", r);
+    seen.insert(row_perm(r));
+  }
+  CHECK(seen.size() == 64, "row_perm is not a bijection on 0..63");
+  for (int t = 0; t < 2; ++t)
+    for (int h = 0; h < 2; ++h)
+      for (int reg = 0; reg < 16; ++reg)
+        CHECK(row_perm(32 * t + acc_row(reg, h)) == 32 * t + 16 * h + reg, "row_perm t %d h %d reg %d", t, h, reg);
+  for (int c = 0; c < 16; ++c)
+    for (int u = 0; u < 4; ++u)
+      CHECK(row_perm(4 * row_perm_src_chunk(c) + u) == 4 * c + u, "DMA chunk %d element %d", c, u);
+}
+
 int main() {
+  check_row_perm();
   check_tile_order();
   check_swizzle<64>();
   check_swizzle<128>();
