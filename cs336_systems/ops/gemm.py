@@ -110,9 +110,10 @@ def _ok(a, b, ta, tb) -> bool:
     return a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and ops().gemm_ok(a, b, ta, tb)
 
 
-def _select(kind, a, b, out, blas, lt, cs336, dw: bool = False) -> str:
+def _select(kind, a, b, out, blas, lt, cs336, dw: bool = False, extra: dict | None = None) -> str:
     """Implementation for this call: ``lt``/``hip`` modes force theirs where it applies, ``best``
-    times the applicable ones (``None`` = not applicable), ``blas`` is hipBLASLt's default."""
+    times the applicable ones (``None`` = not applicable) plus ``extra`` (name -> launcher, best
+    mode only), ``blas`` is hipBLASLt's default."""
     mode = _mode(dw)
     if mode == "lt" and lt is not None:
         return "lt"
@@ -124,6 +125,7 @@ def _select(kind, a, b, out, blas, lt, cs336, dw: bool = False) -> str:
             cands["lt"] = lt
         if cs336 is not None:
             cands["cs336"] = cs336
+        cands.update(extra or {})
         return _pick(kind, a, b, out, cands) if len(cands) > 1 else "blas"
     return "blas"
 
@@ -185,6 +187,30 @@ def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None =
     return out if out is not None else r
 
 
+SPLITK_MAX_OUT = 16 << 20  # output elements up to which split-K candidates are timed (best mode)
+
+
+def _splitk_cands(a3_of, b3_of, k: int, m: int, n: int, out: torch.Tensor | None) -> dict:
+    """Split-K candidates for a long-K, small-output fp32 weight gradient: the token dimension cut
+    into S slices computed as one strided batched GEMM (S x more output tiles to spread over the
+    256 CUs) whose fp32 partials are summed into the result. The o-projection dW (1600 x 1600 out,
+    24576 tokens) fills only ~40 macro-tiles of 256 x 256 without it. ``a3_of(S)`` / ``b3_of(S)``
+    give the (S, m, k/S) and (S, k/S, n) views."""
+    if m * n > SPLITK_MAX_OUT or os.environ.get("CS336_SPLITK", "1") == "0":
+        return {}
+    res = {}
+    for sk in (2, 4, 8):
+        if k % sk or (k // sk) % 64:
+            continue
+
+        def run(sk=sk):
+            part = torch.bmm(a3_of(sk), b3_of(sk), out_dtype=torch.float32)
+            return torch.sum(part, dim=0, out=out) if out is not None else part.sum(0)
+
+        res[f"splitk{sk}"] = run
+    return res
+
+
 def mm_dyt_fp32(dyt: torch.Tensor, x: torch.Tensor, x_is_t: bool, out: torch.Tensor | None = None) -> torch.Tensor:
     """Weight gradient ``dyt @ x`` (``x_is_t``: ``dyt @ x.T``, x holding Xᵀ) with an fp32 result,
     from a token-contiguous ``dYᵀ`` (N_out, tokens). hipBLASLt default pick; ``best`` mode also times
@@ -204,7 +230,16 @@ def mm_dyt_fp32(dyt: torch.Tensor, x: torch.Tensor, x_is_t: bool, out: torch.Ten
     else:
         lt = (lambda: ops().lt_gemm_out(dyt, x, False, x_is_t, out)) if lt_ok else None
         cs = (lambda: ops().gemm_out(dyt, x, False, x_is_t, out, False, 0, 0, 0)) if _ok(dyt, x, False, x_is_t) else None
-    r = {"blas": blas, "lt": lt, "cs336": cs}[_select("dyt32" + ("t" if x_is_t else "n"), dyt, x, out, blas, lt, cs, dw=True)]()
+    m, k = dyt.shape
+    n = b.shape[1]
+    if x_is_t:  # x = Xᵀ (n, k): slice s is x[:, s*kc:(s+1)*kc]ᵀ
+        b3_of = lambda sk: x.view(n, sk, k // sk).permute(1, 2, 0)  # noqa: E731
+    else:  # x (k, n) token-major
+        b3_of = lambda sk: x.view(sk, k // sk, n)  # noqa: E731
+    a3_of = lambda sk: dyt.view(m, sk, k // sk).permute(1, 0, 2)  # noqa: E731
+    extra = _splitk_cands(a3_of, b3_of, k, m, n, out) if _mode(True) == "best" and dyt.is_contiguous() and (x.is_contiguous()) else {}
+    impls = {"blas": blas, "lt": lt, "cs336": cs, **extra}
+    r = impls[_select("dyt32" + ("t" if x_is_t else "n"), dyt, x, out, blas, lt, cs, dw=True, extra=extra)]()
     return out if out is not None else r
 
 
@@ -231,5 +266,12 @@ def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = Non
     else:
         lt = (lambda: ops().lt_gemm_out(dy, x, True, False, out)) if lt_ok else None
         cs = (lambda: ops().gemm_out(dy, x, True, False, out, False, 0, 0, 0)) if _ok(dy, x, True, False) else None
-    r = {"blas": blas, "lt": lt, "cs336": cs}[_select("tn32", dy, x, out, blas, lt, cs, dw=True)]()
+    k, m = dy.shape
+    n = x.shape[1]
+    extra = {}
+    if _mode(True) == "best" and dy.is_contiguous() and x.is_contiguous():
+        extra = _splitk_cands(lambda sk: dy.view(sk, k // sk, m).transpose(1, 2), lambda sk: x.view(sk, k // sk, n),
+                              k, m, n, out)
+    impls = {"blas": blas, "lt": lt, "cs336": cs, **extra}
+    r = impls[_select("tn32", dy, x, out, blas, lt, cs, dw=True, extra=extra)]()
     return out if out is not None else r
