@@ -183,11 +183,22 @@ def mm_tn_fp32_xt(dy: torch.Tensor, xt: torch.Tensor, out: torch.Tensor | None =
         blas = lambda: torch.mm(dy.t(), xt.t(), out_dtype=torch.float32, out=out)  # noqa: E731
         lt = lambda: ops().lt_gemm_out(dy, xt, True, True, out)  # noqa: E731
     use_lt = _mode(True) in ("lt", "best") and _lt_ok(dy, xt) and (out is None or out.stride(1) == 1)
-    r = (lt if use_lt and _select("tt32", dy, xt, out, blas, lt, None, dw=True) == "lt" else blas)()
+    if not use_lt:
+        r = blas()
+        return out if out is not None else r
+    extra = {}
+    if _mode(True) == "best" and dy.is_contiguous() and xt.is_contiguous():
+        k, m = dy.shape
+        n = xt.shape[0]
+        extra = _splitk_cands(lambda sk: dy.view(sk, k // sk, m).transpose(1, 2),
+                              lambda sk: xt.view(n, sk, k // sk).permute(1, 2, 0), k, m, n, out)
+    impls = {"blas": blas, "lt": lt, **extra}
+    r = impls[_select("tt32", dy, xt, out, blas, lt, None, dw=True, extra=extra)]()
     return out if out is not None else r
 
 
-SPLITK_MAX_OUT = 16 << 20  # output elements up to which split-K candidates are timed (best mode)
+SPLITK_MAX_OUT = 32 << 20  # output elements up to which split-K candidates are timed (best mode)
+SPLITK_MAX_PARTIAL_BYTES = 512 << 20  # fp32 partials of one split-K candidate
 
 
 def _splitk_cands(a3_of, b3_of, k: int, m: int, n: int, out: torch.Tensor | None) -> dict:
@@ -196,11 +207,11 @@ def _splitk_cands(a3_of, b3_of, k: int, m: int, n: int, out: torch.Tensor | None
     256 CUs) whose fp32 partials are summed into the result. The o-projection dW (1600 x 1600 out,
     24576 tokens) fills only ~40 macro-tiles of 256 x 256 without it. ``a3_of(S)`` / ``b3_of(S)``
     give the (S, m, k/S) and (S, k/S, n) views."""
-    if m * n > SPLITK_MAX_OUT or os.environ.get("CS336_SPLITK", "1") == "0":
+    if m * n > int(os.environ.get("CS336_SPLITK_MAX_OUT", SPLITK_MAX_OUT)) or os.environ.get("CS336_SPLITK", "1") == "0":
         return {}
     res = {}
     for sk in (2, 4, 8):
-        if k % sk or (k // sk) % 64:
+        if k % sk or (k // sk) % 64 or sk * m * n * 4 > SPLITK_MAX_PARTIAL_BYTES:
             continue
 
         def run(sk=sk):

@@ -127,7 +127,7 @@ def test_model_step_with_hip_gemm_matches_blas(monkeypatch):
         torch.testing.assert_close(g_hip[n] / scale, g_ref[n] / scale, rtol=0, atol=2e-2, msg=n)
 
 
-@pytest.mark.parametrize("kind", ["dyt_n", "dyt_t", "tn"])
+@pytest.mark.parametrize("kind", ["dyt_n", "dyt_t", "tn", "tt"])
 def test_best_mode_splitk_weight_gradients(monkeypatch, kind):
     """best mode's split-K candidates (token dim cut into S slices, one strided batched GEMM, fp32
     partials summed) match an fp32 reference, written into a strided bucket-like view."""
@@ -145,6 +145,11 @@ def test_best_mode_splitk_weight_gradients(monkeypatch, kind):
         k, m = dy.shape
         cands = gemm._splitk_cands(lambda sk: dy.view(sk, k // sk, m).transpose(1, 2), lambda sk: x.view(sk, k // sk, n_in),
                                    k, m, n_in, out)
+    elif kind == "tt":
+        k, m = dy.shape
+        xt = x.t().contiguous()
+        cands = gemm._splitk_cands(lambda sk: dy.view(sk, k // sk, m).transpose(1, 2),
+                                   lambda sk: xt.view(n_in, sk, k // sk).permute(1, 2, 0), k, m, n_in, out)
     else:
         dyt = dy.t().contiguous()
         m, k = dyt.shape
@@ -164,6 +169,8 @@ def test_best_mode_splitk_weight_gradients(monkeypatch, kind):
     out.zero_()
     if kind == "tn":
         gemm.mm_tn_fp32(dy, x, out=out)
+    elif kind == "tt":
+        gemm.mm_tn_fp32_xt(dy, x.t().contiguous(), out=out)
     elif kind == "dyt_t":
         gemm.mm_dyt_fp32(dy.t().contiguous(), x.t().contiguous(), True, out=out)
     else:

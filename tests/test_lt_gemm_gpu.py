@@ -158,5 +158,5 @@ def test_best_mode_times_cs336_gemm_where_it_applies(monkeypatch):
     for key, times in timed.items():
         # fp32 weight gradients also time the split-K candidates (gemm._splitk_cands)
         assert {"blas", "lt", "cs336"} <= set(times), (key, times)
-        assert all(t in ("blas", "lt", "cs336") or (key[0] in ("tn32", "dyt32n", "dyt32t") and t.startswith("splitk")) for t in times), (key, times)
+        assert all(t in ("blas", "lt", "cs336") or (key[0] in ("tn32", "tt32", "dyt32n", "dyt32t") and t.startswith("splitk")) for t in times), (key, times)
         assert gemm.gemm_choices()[key] in times
