@@ -21,14 +21,25 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
+
+from cs336_systems.rccl_env import apply_multi_gpu_env  # noqa: E402  (torch-free)
+
+if __name__ == "__main__":
+    # stream-K grid cap + RCCL channel cap for multi-rank runs, set before torch loads hipBLASLt/RCCL
+    # (cs336_systems/rccl_env.py, profiles/r3_coresidency.md)
+    _CORES_ENV = apply_multi_gpu_env(int(os.environ.get("WORLD_SIZE", "1")))
+else:
+    _CORES_ENV = {}
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 METRIC = "tokens/sec/node GPT-2-XL bf16 DDP"
 BASELINE_VALUE = None  # the reference publishes no number
@@ -91,6 +102,13 @@ def parse(argv=None):
     )
     ap.add_argument("--graphs", action="store_true", help="1 GPU: replay forward+backward from one captured HIP graph")
     ap.add_argument(
+        "--comm-sweep-mb",
+        type=float,
+        nargs="*",
+        default=[1, 10, 100, 1024],
+        help="N > 1: after the timed steps, fp32 all-reduce sweep (5 warmup + 5 timed each) added to the JSON's dist block",
+    )
+    ap.add_argument(
         "--tunableop",
         default="auto",
         choices=["auto", "off", "use", "tune"],
@@ -124,6 +142,41 @@ def setup_tunableop(mode: str, rank: int) -> str | None:
     return mode
 
 
+def self_launch(n: int, argv: list[str]) -> int:
+    """``python bench.py --gpus N`` without a launcher: run the same command under
+    ``torch.distributed.run`` with N ranks on this node (127.0.0.1 rendezvous) and return its exit
+    code. Called before anything touches the GPU; the ranks are child processes (no exec)."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    log(f"bench.py --gpus {n} without WORLD_SIZE: launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd)
+
+
+def comm_sweep(sizes_mb, device, world) -> list[dict]:
+    """The reference's all-reduce microbenchmark (``distributed_communication_single.py:28-148``,
+    handout p.26: fp32, 5 warmup + timed calls) on the job's own process group, after the timed
+    steps: per size the max over ranks of the mean time, algorithm and bus bandwidth."""
+    from cs336_systems.bench.collectives import _busbw_factor, run_collective
+
+    rows = []
+    for mb in sizes_mb:
+        nbytes = int(mb * 2**20)
+        t = run_collective("all_reduce", nbytes, device, warmup=5, iters=5)
+        on_dev = dist.get_backend() == "nccl"
+        tt = torch.tensor([t], dtype=torch.float64, device=device if on_dev else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+        algbw = nbytes / t / 1e9
+        rows.append({"size_mb": mb, "ms": round(t * 1e3, 4), "algbw_gbs": round(algbw, 3),
+                     "busbw_gbs": round(algbw * _busbw_factor("all_reduce", world), 3)})
+        if device.type == "cuda":
+            torch.cuda.empty_cache()
+    return rows
+
+
 def dist_diagnostics(ddp_model, comm_wait_ms, device, world) -> dict:
     """What a multi-GPU run needs to be diagnosable from its own JSON line: exposed communication
     per step (max over ranks), the bucket layout, the process group as the ranks see it, the
@@ -149,7 +202,9 @@ def dist_diagnostics(ddp_model, comm_wait_ms, device, world) -> dict:
         d["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
     except Exception as e:  # noqa: BLE001 - diagnostic only
         d["rccl_version"] = f"unavailable ({type(e).__name__})"
-    d["env"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith(("NCCL_", "RCCL_", "HSA_", "TORCH_NCCL_"))}
+    d["env"] = {k: v for k, v in sorted(os.environ.items())
+                if k.startswith(("NCCL_", "RCCL_", "HSA_", "TORCH_NCCL_", "TENSILE_STREAMK"))}
+    d["coresidency_caps"] = dict(_CORES_ENV)
     if buckets and world > 1 and device.type == "cuda" and dist.get_backend() == "nccl":
         n = int(max(mbs) * 2**20 // 4)
         buf = torch.ones(n, dtype=torch.float32, device=device)
@@ -170,10 +225,15 @@ def dist_diagnostics(ddp_model, comm_wait_ms, device, world) -> dict:
 
 
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return self_launch(args.gpus, argv)  # never a mislabeled 1-GPU number
+    world = int(world_env or 1)
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world} (launch N ranks for --gpus N)")
+        return 2
     rank = int(os.environ.get("RANK", "0"))
 
     os.environ["CS336_GEMM"] = args.gemm  # read per call by cs336_systems.ops.gemm
@@ -376,6 +436,8 @@ def main(argv=None):
     out["config"]["gemm_selection"] = f"tunableop:{tmode}" if tmode else gsel if device.type == "cuda" else "torch cpu"
     if world > 1 or zero:
         out["dist"] = dist_diagnostics(ddp_model, comm_wait_ms, device, world)
+        if world > 1 and args.comm_sweep_mb:
+            out["dist"]["allreduce_sweep_fp32"] = comm_sweep(args.comm_sweep_mb, device, world)
     if tmode == "tune" and rank == 0:
         import torch.cuda.tunable as tunable
 
@@ -387,6 +449,8 @@ def main(argv=None):
         ch = gemm_choices()
         with open(rep, "w") as fh:
             json.dump([{"key": str(k), "pick": ch.get(k), "ms": v} for k, v in gemm_timings().items()], fh, indent=1)
+        with open(rep + ".lt.json", "w") as fh:  # autotuned hipBLASLt candidates (scripts/gemm_table.py pins)
+            json.dump(sorted(torch.ops.cs336.lt_gemm_picks()), fh, indent=1)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

@@ -41,9 +41,15 @@ _SHADOW_T_GEN = "_cs336_bf16t_gen"  # shadow generation the Wᵀ was written at
 # ------------------------------------------------------------------------------------------
 # grouped storage
 # ------------------------------------------------------------------------------------------
+_GROUP_SEQ = 0
+
+
 @torch.no_grad()
 def group_params_(params: list[nn.Parameter]) -> torch.Tensor:
     """Re-home ``params`` (2-D, same width/dtype/device) as consecutive row blocks of one tensor."""
+    global _GROUP_SEQ
+    _GROUP_SEQ += 1
+    gid = _GROUP_SEQ
     d_in = params[0].shape[1]
     rows = sum(p.shape[0] for p in params)
     base = torch.empty(rows, d_in, dtype=params[0].dtype, device=params[0].device)
@@ -53,6 +59,9 @@ def group_params_(params: list[nn.Parameter]) -> torch.Tensor:
         base[off : off + n].copy_(p.data)
         p.data = base[off : off + n]
         off += n
+        # group tag: DDP bucketing keeps a group together even after another wrapper (ZeRO-1's flat
+        # buffers) has moved every parameter into one storage
+        p._cs336_group = gid
     return base
 
 
@@ -402,7 +411,9 @@ class FusedLinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         if x2.dtype != cdt:
             x2 = x2.to(cdt)
-        y = gemm.mm_nt(x2, w)
+        # (a fused consumer -- SwiGLUFFNFn -- may supply its own GEMM with an epilogue)
+        mm = getattr(ctx, "mm_override", None) or gemm.mm_nt
+        y = mm(x2, w)
         # For wide projections (N_out >= r * K_in, e.g. W1|W3: 12800 vs 1600) save Xᵀ instead of X:
         # the weight-gradient GEMM dYᵀX then reads both operands token-contiguous, which hipBLASLt
         # runs 1.4x faster on MI355X (profiles/r1_gemm_dw_layouts.json), for one small transpose.
@@ -468,7 +479,7 @@ class FusedLinearFn(torch.autograd.Function):
         if dy2.dtype != w.dtype:
             dy2 = dy2.to(w.dtype)
         dx = dw_parts = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and not getattr(ctx, "skip_dx", False):
             if ctx.w_t:  # w holds Wᵀ (K_in, N_out), made on the side stream (or in-stream under capture)
                 if ctx.wt_event is not None:
                     main = torch.cuda.current_stream(dy2.device)
@@ -593,6 +604,93 @@ class AttentionCore(torch.autograd.Function):
             hip.fa_bwd_into(do, qk[:, :H], qk[:, H:], v, o, lse, True, ctx.scale, dqk[:, :H], dqk[:, H:], dv)
             hip.rope_into(dqk, cos, sin, pos, True, dqk)
         return dqkv, None, None, None, None, None
+
+
+class _SubCtx:
+    """Stand-in for an autograd ctx, so FusedLinearFn's forward/backward run as one stage of a
+    larger Function (SwiGLUFFNFn) and keep all their logic: bf16/Wᵀ shadows, Xᵀ / dYᵀ layouts,
+    fp32 dW written straight into the DDP bucket."""
+
+    def __init__(self, needs_input_grad):
+        self.needs_input_grad = tuple(needs_input_grad)
+        self._saved = ()
+
+    def save_for_backward(self, *ts):
+        self._saved = ts
+
+    @property
+    def saved_tensors(self):
+        return self._saved
+
+
+def swiglu_fused_enabled() -> bool:
+    """SwiGLU gate inside the gemm8 epilogues (CS336_SWIGLU_FUSED=0: separate HIP SwiGLU kernels)."""
+    return os.environ.get("CS336_SWIGLU_FUSED", "1") != "0"
+
+
+class SwiGLUFFNFn(torch.autograd.Function):
+    """``w2(silu(w1 x) * w3 x)`` on the grouped W1|W3 layout with the gate fused into the GEMMs
+    (``model.py:389-397``; kernels in ``csrc/gemm/gemm8.hip``):
+
+    * forward: ONE kernel writes y = x·[W1;W3]ᵀ (saved) and h = silu(a)·b; then h·W2ᵀ;
+    * backward: dW2 = dYᵀ·h, then ONE kernel computes dh = dY·W2 in registers and writes
+      [da|db] = [dh·b·silu'(a) | dh·silu(a)] from the saved y (dh never reaches memory); then the
+      W1|W3 input and weight gradients from [da|db].
+
+    Removes both SwiGLU elementwise passes (read 2·d_ff + write d_ff, and read 3·d_ff + write 2·d_ff
+    activations per token). Shapes the kernel does not take fall back to GEMM + SwiGLU kernel inside
+    the same Function."""
+
+    @staticmethod
+    def forward(ctx, x, w1, w3, w2):
+        c13 = _SubCtx((True, False, w1.requires_grad, w3.requires_grad))
+        box = {}
+
+        def mm13(x2, w):
+            half = w.shape[0] // 2
+            if gemm.gemm8_ok(x2, w, 1, half):
+                y2, box["h"] = gemm.gemm8_swiglu_fwd(x2, w)
+            else:
+                y2 = gemm.mm_nt(x2, w)
+                box["h"] = _hip().swiglu_fused_fwd(y2)
+            return y2
+
+        c13.mm_override = mm13
+        y = FusedLinearFn.forward(c13, x, None, w1, w3)
+        h = box["h"].view(*x.shape[:-1], -1)
+        c2 = _SubCtx((True, False, w2.requires_grad))
+        out = FusedLinearFn.forward(c2, h, None, w2)
+        ctx.c13, ctx.c2 = c13, c2
+        ctx.save_for_backward(y)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (y,) = ctx.saved_tensors
+        c13, c2 = ctx.c13, ctx.c2
+        c2.skip_dx = True  # W2 stage: weight gradient only; its input gradient is fused below
+        _, _, dw2 = FusedLinearFn.backward(c2, dout)
+        h2, w2s = c2.saved_tensors
+        dy2 = dout.reshape(-1, dout.shape[-1])
+        if dy2.dtype != w2s.dtype:
+            dy2 = dy2.to(w2s.dtype)
+        y2 = y.reshape(-1, y.shape[-1])
+        half = y2.shape[1] // 2
+        if c2.w_t and c2.wt_event is not None:
+            main = torch.cuda.current_stream(dy2.device)
+            main.wait_event(c2.wt_event)
+            w2s.record_stream(main)
+        if c2.w_t and gemm.gemm8_ok(dy2, w2s, 2, half) and gemm._aligned_rows(y2):
+            dab = gemm.gemm8_swiglu_bwd(dy2, w2s, y2)
+        else:
+            dh = gemm.mm_nt(dy2, w2s) if c2.w_t else gemm.mm_nn(dy2, w2s)
+            dab = _hip().swiglu_fused_bwd(dh.contiguous(), y2)
+        dx, _, dw1, dw3 = FusedLinearFn.backward(c13, dab.view(*y.shape))
+        # the stages' saved tensors are plain attributes (not SavedVariables): drop them now, or
+        # every layer's h / Xᵀ would live until the whole graph is freed (+18 GiB peak on XL)
+        c13._saved = c2._saved = ()
+        ctx.c13 = ctx.c2 = None
+        return dx, dw1, dw3, dw2
 
 
 class SwiGLUGate(torch.autograd.Function):

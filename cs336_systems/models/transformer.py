@@ -168,12 +168,24 @@ class SwiGLU(nn.Module):
         self.w2 = Linear(d_ff, d_model, device, dtype)
         self.w3 = Linear(d_model, d_ff, device, dtype)
 
+    def _fused_ffn_ok(self, x) -> bool:
+        """bf16 compute (autocast or bf16 weights) on the HIP path and a tiling gemm8 takes: tokens a
+        multiple of 256, d_ff of 160 or 128; anything else runs GEMM + the separate gate kernel."""
+        cdt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else self.w1.weight.dtype
+        tokens = x.numel() // x.shape[-1]
+        d_ff, d_model = self.w1.weight.shape
+        return (cdt == torch.bfloat16 and tokens % 256 == 0 and (d_ff % 160 == 0 or d_ff % 128 == 0)
+                and d_model % 64 == 0 and ops.ext_available())
+
     def group_(self) -> None:
         """Store w1 and w3 as one (2*d_ff, d_model) block so the gate projections are one GEMM."""
         fused.group_params_([self.w1.weight, self.w3.weight])
 
     def forward(self, x):
         if x.is_cuda and ops.use_hip(x) and fused.grouped_view([self.w1.weight, self.w3.weight]) is not None:
+            if fused.swiglu_fused_enabled() and self._fused_ffn_ok(x):
+                # gate in the GEMM epilogues: y/h from one kernel, [da|db] from the W2 input-grad GEMM
+                return fused.SwiGLUFFNFn.apply(x, self.w1.weight, self.w3.weight, self.w2.weight)
             y = fused.fused_linear(x, self.w1.weight, self.w3.weight)  # [a | b], (..., 2*d_ff)
             return self.w2(fused.SwiGLUGate.apply(y))
         return self.w2(ops.silu_mul(self.w1(x), self.w3(x)))

@@ -59,6 +59,42 @@ def _mode(dw: bool = False) -> str:
 
 
 _BEST: dict = {}
+_TABLE: dict | None = None
+TABLE_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "gemm_table_mi355x.json")
+
+
+def selection_table() -> dict:
+    """Committed per-problem picks (``cs336_systems/tuning/gemm_table_mi355x.json``, produced on
+    MI355X by ``scripts/gemm_table.py`` from a ``CS336_GEMM_REPORT``): problem key -> implementation.
+    Every rank and every box loads the same file, so ``best`` mode picks the same kernels everywhere
+    and times nothing for the shapes it covers. ``CS336_GEMM_TABLE=0`` ignores it, ``=path`` loads
+    another file."""
+    global _TABLE
+    if _TABLE is None:
+        path = os.environ.get("CS336_GEMM_TABLE", TABLE_FILE)
+        _TABLE = {}
+        pins: list = []
+        if path != "0" and os.path.exists(path):
+            import json
+
+            with open(path) as f:
+                doc = json.load(f)
+            _TABLE = dict(doc.get("entries", {}))
+            pins = list(doc.get("lt_pins", []))
+        if ext_available():
+            # the autotuned hipBLASLt op takes the committed candidate (no per-process timing), and in a
+            # multi-rank job an unpinned problem takes the heuristic's first choice instead of timing
+            for pin in pins:
+                m, n, k, at, bt, oc, idx, name = pin.split(",", 7)
+                ops().lt_gemm_pin(int(m), int(n), int(k), at == "1", bt == "1", int(oc), int(idx), name)
+            ops().lt_gemm_set_no_timing(_multi_rank())
+    return _TABLE
+
+
+def _multi_rank() -> bool:
+    import torch.distributed as dist
+
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
 def _time_ms(fn, reps: int = 5) -> float:
@@ -73,14 +109,26 @@ def _time_ms(fn, reps: int = 5) -> float:
 
 
 def _pick(kind: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None, cands: dict) -> str:
-    """``best`` mode: the fastest of ``cands`` (name -> zero-arg launcher) for this problem, timed
-    once with HIP events on the current stream and cached ("blas" on near-ties, within 3 %, and
-    while a HIP graph is being captured, where nothing can be timed)."""
+    """``best`` mode: the committed table's pick for this problem (:func:`selection_table`); for a
+    problem the table does not cover, the fastest of ``cands`` (name -> zero-arg launcher), timed
+    once with HIP events on the current stream and cached ("blas" on near-ties, within 3 %). Never
+    timed while a HIP graph is being captured, nor in a multi-rank job: per-process timing races
+    could give ranks different kernels, and a timing run inside a DDP backward would sit beside
+    in-flight all-reduces -- unseen problems run hipBLASLt's default there."""
     key = (kind, tuple(a.shape), a.stride(), tuple(b.shape), b.stride(),
            None if out is None else (out.dtype, out.stride()))
     hit = _BEST.get(key)
     if hit is None:
+        t = selection_table().get(str(key))
+        if t is not None and t in cands:
+            _BEST[key] = t
+            _BEST_TIMES[key] = {"table": t}
+            return t
         if torch.cuda.is_current_stream_capturing():
+            return "blas"
+        if _multi_rank():
+            _BEST[key] = "blas"
+            _BEST_TIMES[key] = {"untimed_multi_rank": "blas"}
             return "blas"
         times = {name: _time_ms(fn) for name, fn in cands.items()}
         best = min(times, key=times.get)
@@ -115,6 +163,8 @@ def _select(kind, a, b, out, blas, lt, cs336, dw: bool = False, extra: dict | No
     times the applicable ones (``None`` = not applicable) plus ``extra`` (name -> launcher, best
     mode only), ``blas`` is hipBLASLt's default."""
     mode = _mode(dw)
+    if mode in ("lt", "best"):
+        selection_table()  # loads the committed picks / lt pins once
     if mode == "lt" and lt is not None:
         return "lt"
     if mode == "hip" and cs336 is not None:
@@ -130,14 +180,66 @@ def _select(kind, a, b, out, blas, lt, cs336, dw: bool = False, extra: dict | No
     return "blas"
 
 
+def _aligned_rows(t: torch.Tensor) -> bool:
+    return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0
+
+
+def gemm8_ok(x: torch.Tensor, w: torch.Tensor, epi: int = 0, half: int = 0) -> bool:
+    """Whether the gemm8 NT kernel (``csrc/gemm/gemm8.hip``) takes ``x @ w.T``: bf16, row-major with
+    16-B aligned rows, M % 256, K % 64, N a multiple of 320 or 256 (epi 1: half of 160 or 128)."""
+    return (
+        x.is_cuda
+        and x.dtype == torch.bfloat16
+        and w.dtype == torch.bfloat16
+        and _aligned_rows(x)
+        and _aligned_rows(w)
+        and x.shape[1] == w.shape[1]
+        and ext_available()
+        and ops().gemm8_ok(x.shape[0], w.shape[0], x.shape[1], epi, half)
+    )
+
+
+def gemm8(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    out = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=torch.bfloat16)
+    ops().gemm8(x, w, out, 0, 0, None, None, 0)
+    return out
+
+
+def gemm8_swiglu_fwd(x: torch.Tensor, w13: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """``y = x @ [w1; w3].T`` and ``h = silu(y_a) * y_b`` from one kernel (SwiGLU gate in the GEMM
+    epilogue): returns (y, h)."""
+    half = w13.shape[0] // 2
+    y = torch.empty(x.shape[0], 2 * half, device=x.device, dtype=torch.bfloat16)
+    h = torch.empty(x.shape[0], half, device=x.device, dtype=torch.bfloat16)
+    ops().gemm8(x, w13, y, 1, 0, h, None, half)
+    return y, h
+
+
+def gemm8_swiglu_bwd(dy: torch.Tensor, w2t: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """``[da | db]`` from ``dh = dy @ w2t.T`` (never stored) and the saved ``y = [a | b]``: the W2
+    input gradient with the SwiGLU backward in its epilogue."""
+    half = w2t.shape[0]
+    out = torch.empty(dy.shape[0], 2 * half, device=dy.device, dtype=torch.bfloat16)
+    ops().gemm8(dy, w2t, out, 2, 0, None, y, half)
+    return out
+
+
 def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """``x @ w.T`` (forward of a linear layer)."""
-    if _mode() == "blas":
+    """``x @ w.T`` (forward of a linear layer; the input gradient through a Wᵀ shadow)."""
+    mode = _mode()
+    if mode == "blas":
         return torch.mm(x, w.t())
     blas = lambda: torch.mm(x, w.t())  # noqa: E731
     lt = (lambda: ops().lt_gemm(x, w, False, True, torch.bfloat16)) if _lt_ok(x, w) else None
+    g8 = (lambda: gemm8(x, w)) if gemm8_ok(x, w) else None
+    if mode == "hip":  # the hand-written kernels: gemm8 where it applies, else the older cs336 GEMM
+        cs = g8 if g8 is not None else ((lambda: ops().gemm(x, w, False, True, torch.bfloat16, 0, 0, 0))
+                                        if _ok(x, w, False, True) else None)
+        return (cs or blas)()
     cs = (lambda: ops().gemm(x, w, False, True, torch.bfloat16, 0, 0, 0)) if _ok(x, w, False, True) else None
-    return {"blas": blas, "lt": lt, "cs336": cs}[_select("nt", x, w, None, blas, lt, cs)]()
+    extra = {"g8": g8} if g8 is not None else {}
+    impls = {"blas": blas, "lt": lt, "cs336": cs, **extra}
+    return impls[_select("nt", x, w, None, blas, lt, cs, extra=extra)]()
 
 
 def mm_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -210,8 +312,13 @@ def _splitk_cands(a3_of, b3_of, k: int, m: int, n: int, out: torch.Tensor | None
     if m * n > int(os.environ.get("CS336_SPLITK_MAX_OUT", SPLITK_MAX_OUT)) or os.environ.get("CS336_SPLITK", "1") == "0":
         return {}
     res = {}
+    # the partials of the candidate being timed are extra memory at the selection step (first
+    # step, inside backward): time a candidate only with room to spare
+    free = torch.cuda.mem_get_info()[0] if torch.cuda.is_available() else 0
     for sk in (2, 4, 8):
         if k % sk or (k // sk) % 64 or sk * m * n * 4 > SPLITK_MAX_PARTIAL_BYTES:
+            continue
+        if sk * m * n * 4 + (4 << 30) > free:
             continue
 
         def run(sk=sk):

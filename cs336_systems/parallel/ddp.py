@@ -59,15 +59,22 @@ def _unique_params(module: nn.Module) -> list[nn.Parameter]:
 
 def bucket_params(params: list[nn.Parameter], cap_bytes: float) -> list[list[nn.Parameter]]:
     """Greedy buckets over ``reversed(params)`` (≈ backward order) of at most ``cap_bytes``, never
-    mixing dtypes/devices. Parameters that share one storage (the fused QKV / W1|W3 layout of
-    models/fused.py) form an indivisible unit laid out in storage order, so the grouped dW GEMM can
-    write all of them into one contiguous region of the bucket."""
-    by_storage: dict[int, list[nn.Parameter]] = {}
+    mixing dtypes/devices. The parameters of one fused group (the QKV / W1|W3 layout of
+    models/fused.py, tagged ``_cs336_group``) form an indivisible unit laid out in storage order, so
+    the grouped dW GEMM can write all of them into one contiguous region of the bucket. Untagged
+    parameters are their own unit, even if they share a storage (e.g. after ZeRO-1 re-homed the whole
+    model into one flat buffer: a storage key would then make the model a single bucket)."""
+
+    def unit_key(p):
+        g = getattr(p, "_cs336_group", None)
+        return ("g", g) if g is not None else ("p", id(p))
+
+    by_storage: dict = {}
     for p in params:
-        by_storage.setdefault(p.untyped_storage().data_ptr(), []).append(p)
+        by_storage.setdefault(unit_key(p), []).append(p)
     units, seen = [], set()
     for p in reversed(params):
-        key = p.untyped_storage().data_ptr()
+        key = unit_key(p)
         if key in seen:
             continue
         seen.add(key)

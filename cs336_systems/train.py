@@ -161,10 +161,11 @@ def train(cfg: TrainConfig) -> dict:
     shadows = dev.type == "cuda" and cfg.dtype == "bf16"
     zero = cfg.ddp == "zero"  # ZeRO-2: the wrapper owns the (sharded) optimizer, built after loading
     tp = cfg.tensor_parallel and world > 1  # TP: shard after loading the full weights, then build the optimizer
-    if zero or tp:
+    if zero or tp or cfg.sharded:
+        # ZeRO-1 is built after the DDP wrap: ShardedOptimizer re-homes every parameter into one flat
+        # buffer per dtype, and DDPBucketed would then see the whole model as one storage unit (one
+        # bucket, no overlap) if it were wrapped afterwards
         opt = None
-    elif cfg.sharded:
-        opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw)
     else:
         opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)
 
@@ -192,6 +193,10 @@ def train(cfg: TrainConfig) -> dict:
             load_optimizer_state(path, opt, map_location=dev)
     else:
         ddp = model if use_graphs else wrap_ddp(model, cfg.ddp, bucket_size_mb=cfg.bucket_mb)
+        if cfg.sharded:
+            opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw)
+            if path is not None:
+                load_optimizer_state(path, opt, map_location=dev)
     if isinstance(opt, ShardedOptimizer):
         opt.attach(ddp)  # the in-place parameter all-gather is waited for by the next forward
     graphed = None

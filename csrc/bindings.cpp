@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "cs336/kernels.h"
+#include "../gemm/gemm8.h"
 
 namespace {
 
@@ -766,6 +767,75 @@ void occupy(int64_t n_workgroups, int64_t lds_bytes, double ms, at::Tensor& coun
   cs336::occupy((int)n_workgroups, (int)lds_bytes, ms, counter.data_ptr<int>(), stream());
 }
 
+// co-residency probe (csrc/ops/occupy.hip), on the current stream; state: int32[3]
+void cohort(int64_t n_workgroups, int64_t lds_bytes, double deadline_ms, at::Tensor& state) {
+  check_cuda(state, "state");
+  TORCH_CHECK(state.scalar_type() == at::kInt && state.numel() >= 3 && state.is_contiguous(),
+              "cs336: cohort state must be a contiguous int32[3]");
+  TORCH_CHECK(n_workgroups > 0 && n_workgroups <= 4096 && lds_bytes >= 4 && lds_bytes <= 160 * 1024 &&
+                  deadline_ms > 0 && deadline_ms <= 2000,
+              "cs336: cohort arguments out of range");
+  cs336::cohort((int)n_workgroups, (int)lds_bytes, deadline_ms, state.data_ptr<int>(), stream());
+}
+
+// NT projection GEMM with fused SwiGLU epilogues (csrc/gemm/gemm8.hip), on the current stream.
+//   epi 0: c = a @ b.T                      a (M,K), b (N,K), c (M,N)
+//   epi 1: y = c = a @ [w1; w3].T, h = silu(y[:, :half]) * y[:, half:]     b (2·half, K)
+//   epi 2: dh = a @ b.T (not stored); c = [dh·b·silu'(a) | dh·silu(a)] from y = [a|b]   b (half, K)
+bool gemm8_check(const at::Tensor& t, int64_t rows, int64_t cols, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 && t.stride(1) == 1, "cs336: gemm8 ",
+              what, " must be a row-major bf16 CUDA matrix");
+  TORCH_CHECK(t.size(0) == rows && t.size(1) == cols, "cs336: gemm8 ", what, " shape ", t.sizes(), " expected (", rows,
+              ", ", cols, ")");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "cs336: gemm8 ", what,
+              " rows must be 16-B aligned");
+  return true;
+}
+
+bool gemm8_ok(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t half) {
+  const int fn = cs336::gemm8::pick_fn((int)N, (int)epi, (int)half);
+  return fn != 0 && M % 256 == 0 && K % 64 == 0 && K >= 64 && N % (64 * fn) == 0 && M < (1 << 30);
+}
+
+void gemm8(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, int64_t epi, int64_t fn, const OptT& h,
+           const OptT& y, int64_t half) {
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  gemm8_check(a, M, K, "a");
+  gemm8_check(b, N, K, "b");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "cs336: gemm8 epi");
+  TORCH_CHECK(gemm8_ok(M, N, K, epi, half), "cs336: gemm8 does not take M=", M, " N=", N, " K=", K, " epi=", epi);
+  cs336::gemm8::Args p{};
+  p.a = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  p.b = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  p.lda = a.stride(0);
+  p.ldb = b.stride(0);
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.half = (int)half;
+  if (epi == 0) {
+    gemm8_check(c, M, N, "c");
+  } else if (epi == 1) {
+    TORCH_CHECK(N == 2 * half, "cs336: gemm8 epi 1 needs b = [w1; w3] with 2·half rows");
+    gemm8_check(c, M, N, "y");
+    TORCH_CHECK(h.has_value() && h->defined(), "cs336: gemm8 epi 1 needs h");
+    gemm8_check(*h, M, half, "h");
+    p.h = reinterpret_cast<uint16_t*>(h->data_ptr());
+    p.ldh = h->stride(0);
+  } else {
+    TORCH_CHECK(N == half, "cs336: gemm8 epi 2 needs b with half rows");
+    gemm8_check(c, M, 2 * half, "c = [da|db]");
+    TORCH_CHECK(y.has_value() && y->defined(), "cs336: gemm8 epi 2 needs y");
+    gemm8_check(*y, M, 2 * half, "y");
+    p.y = reinterpret_cast<const uint16_t*>(y->data_ptr());
+    p.ldy = y->stride(0);
+  }
+  p.c = reinterpret_cast<uint16_t*>(c.data_ptr());
+  p.ldc = c.stride(0);
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(cs336::gemm8::launch(p, (int)epi, (int)fn, stream()), "cs336: gemm8 launch (fn ", fn, ")");
+}
+
 TORCH_LIBRARY(cs336, m) {
   m.def(
       "fa_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None, "
@@ -807,6 +877,9 @@ TORCH_LIBRARY(cs336, m) {
       "Tensor(d!)[] shadows, Tensor(e!)[] wts, float lr, float beta1, float beta2, float eps, float weight_decay, "
       "int step) -> ()");
   m.def("occupy(int n_workgroups, int lds_bytes, float ms, Tensor(a!) counter) -> ()");
+  m.def("cohort(int n_workgroups, int lds_bytes, float deadline_ms, Tensor(a!) state) -> ()");
+  m.def("gemm8(Tensor a, Tensor b, Tensor(a!) c, int epi, int fn, Tensor(b!)? h, Tensor? y, int half) -> ()");
+  m.def("gemm8_ok(int M, int N, int K, int epi, int half) -> bool", &gemm8_ok);
   m.def("multi_tensor_scale_(Tensor(a!)[] tensors, Tensor scale) -> ()");
 }
 
@@ -836,5 +909,7 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("adamw_step_t", &adamw_step_t);
   m.impl("multi_tensor_l2norm", &multi_tensor_l2norm);
   m.impl("occupy", &occupy);
+  m.impl("cohort", &cohort);
+  m.impl("gemm8", &gemm8);
   m.impl("multi_tensor_scale_", &multi_tensor_scale_);
 }

@@ -107,6 +107,28 @@ std::string kernel_name(hipblasLtHandle_t h, hipblasLtMatmulAlgo_t& algo) {
 std::mutex g_mu;
 std::unordered_map<Key, Plan, KeyHash> g_plans;
 
+// Committed picks (cs336_systems/tuning/gemm_table_mi355x.json "lt_pins"): problem -> index into the
+// heuristic's candidate list + that candidate's kernel name. A pinned problem takes its candidate
+// without timing (same kernel on every rank and box); a stale pin (name mismatch: another hipBLASLt)
+// is ignored. g_no_timing (multi-rank jobs): an unpinned problem takes the heuristic's first choice
+// instead of timing candidates inside a DDP backward, beside in-flight all-reduces.
+struct PinKey {
+  int64_t m, n, k;
+  bool a_t, b_t;
+  int out;
+  bool operator==(const PinKey& o) const {
+    return m == o.m && n == o.n && k == o.k && a_t == o.a_t && b_t == o.b_t && out == o.out;
+  }
+};
+struct PinHash {
+  size_t operator()(const PinKey& k) const {
+    return std::hash<int64_t>()(k.m * 1000003 + k.n * 10007 + k.k) ^ (size_t(k.a_t) << 1) ^ (size_t(k.b_t) << 2) ^
+           (size_t(k.out) << 3);
+  }
+};
+std::unordered_map<PinKey, std::pair<int, std::string>, PinHash> g_pins;
+bool g_no_timing = false;
+
 int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return v && *v ? std::atoi(v) : dflt;
@@ -180,6 +202,7 @@ void all_data_parallel(hipblasLtHandle_t h, Plan& p, const Key& k, size_t ws_byt
 
 void tune(hipblasLtHandle_t h, Plan& p, const Key& k, const void* a, const void* b, void* out, void* ws, size_t ws_bytes,
           hipStream_t s, bool capturing) {
+  const bool really_capturing = capturing;
   hipblasLtMatmulPreference_t pref;
   LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
   uint64_t wsb = ws_bytes;
@@ -205,12 +228,26 @@ void tune(hipblasLtHandle_t h, Plan& p, const Key& k, const void* a, const void*
   TORCH_CHECK(got > 0, "hipBLASLt: no ", no_sk ? "data-parallel (non-stream-K) " : "", "algorithm for ", k.m, "x",
               k.n, "x", k.k, " among ", got_all, " candidates");
   p.n_cand = got;
+  if (!no_sk) {
+    auto pin = g_pins.find(PinKey{k.m, k.n, k.k, k.a_t, k.b_t, k.out});
+    if (pin != g_pins.end() && pin->second.first < got && names[pin->second.first] == pin->second.second &&
+        res[pin->second.first].workspaceSize <= ws_bytes) {
+      const int i = pin->second.first;
+      p.algo = res[i].algo;
+      p.ws = res[i].workspaceSize;
+      p.kernel = names[i];
+      p.best_idx = i;
+      p.tuned = true;
+      return;
+    }
+    if (g_no_timing) capturing = true;  // heuristic first choice, marked tuned below
+  }
   if (capturing || got == 1) {
     // Cannot time inside a capture: use the heuristic's first choice, retune on the next eager call.
     p.algo = res[0].algo;
     p.ws = res[0].workspaceSize;
     p.kernel = names[0];
-    p.tuned = !capturing;
+    p.tuned = !really_capturing;
     return;
   }
   const int reps = std::max(1, env_int("CS336_LT_REPS", 5));
@@ -341,9 +378,38 @@ std::vector<int64_t> lt_gemm_table() {
   return t;
 }
 
+void lt_gemm_pin(int64_t m, int64_t n, int64_t k, bool a_t, bool b_t, int64_t out_code, int64_t idx,
+                 const std::string& kernel) {
+  std::lock_guard<std::mutex> g(g_mu);
+  g_pins[PinKey{m, n, k, a_t, b_t, int(out_code)}] = {int(idx), kernel};
+}
+
+void lt_gemm_set_no_timing(bool v) {
+  std::lock_guard<std::mutex> g(g_mu);
+  g_no_timing = v;
+}
+
+// "m,n,k,a_t,b_t,out,best_idx,kernel" per tuned problem (the pin list scripts/gemm_table.py commits)
+std::vector<std::string> lt_gemm_picks() {
+  std::lock_guard<std::mutex> g(g_mu);
+  std::vector<std::string> r;
+  for (auto& kv : g_plans) {
+    const Key& k = kv.first;
+    const Plan& p = kv.second;
+    if (!p.tuned || (k.flags & kNoStreamK)) continue;
+    r.push_back(std::to_string(k.m) + "," + std::to_string(k.n) + "," + std::to_string(k.k) + "," +
+                std::to_string(int(k.a_t)) + "," + std::to_string(int(k.b_t)) + "," + std::to_string(k.out) + "," +
+                std::to_string(p.best_idx) + "," + p.kernel);
+  }
+  return r;
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(cs336, m) {
+  m.def("lt_gemm_pin(int m, int n, int k, bool a_t, bool b_t, int out_code, int idx, str kernel) -> ()", &lt_gemm_pin);
+  m.def("lt_gemm_set_no_timing(bool v) -> ()", &lt_gemm_set_no_timing);
+  m.def("lt_gemm_picks() -> str[]", &lt_gemm_picks);
   m.def("lt_gemm(Tensor a, Tensor b, bool a_t, bool b_t, ScalarType out_dtype) -> Tensor");
   m.def("lt_gemm_out(Tensor a, Tensor b, bool a_t, bool b_t, Tensor(a!) out) -> ()");
   m.def("lt_gemm_table() -> int[]", &lt_gemm_table);

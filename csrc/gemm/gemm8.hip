@@ -1,0 +1,445 @@
+// cs336-build: agpr-accumulators
+//
+// "gemm8": the projection GEMMs of the Transformer step in NT form, C = A · Bᵀ with both operands
+// K-major (forward X·Wᵀ; input gradient dY·W read through the Wᵀ shadow the fused AdamW writes),
+// with the SwiGLU gate fused into the epilogues:
+//
+//   EPI 0  C = A·Bᵀ (bf16)
+//   EPI 1  W1|W3 forward: the tile's columns are W1 rows j0.. and the W3 rows half+j0.. , so one tile
+//          holds a and b of the same hidden units; writes y = [a|b] (saved for backward) AND
+//          h = silu(a)·b (the W2 input) -- no separate SwiGLU pass over the 2·d_ff activation
+//   EPI 2  W2 input gradient: dh = dY·W2 is never stored; the epilogue reads the saved a, b and writes
+//          da = dh·b·silu'(a), db = dh·silu(a) into [da|db] (the W1|W3 output gradient)
+//
+// Structure (cdna_hip_programming.md §5 "256² 8-phase template", re-derived for these shapes):
+// * tile 256 × BN (BN = 64·FN: 256 or 320 -- every N of the XL/2.7b projections is a multiple of
+//   320 or 256, d_model 1600 = 5·320), BK = 64, 512 threads = 8 waves as 2 (M) × 4 (N), each wave
+//   128 × 16·FN of v_mfma_f32_16x16x32_bf16 accumulators (AGPRs);
+// * two LDS stages (one K-tile each, ≤ 144 KiB) filled by LDS-DMA (buffer_load … lds, 16 B/lane),
+//   K-major images with the 16-B chunk XOR-swizzled by (row>>1)&7 (conflict-free ds_read_b128 for
+//   the 16x16x32 fragment lane groups; the swizzle goes on the per-lane global source address);
+// * each K-tile runs as 4 phases = the wave's 4 output quadrants (rows 0-63 / 64-127 × the first
+//   FB0 / last FN-FB0 column tiles). Phase = {ds_read its fragments; issue a slice of the K-tile
+//   after next; lgkmcnt(0); s_barrier; MFMA cluster; s_barrier}. The second wave group (waves 4-7,
+//   the partner of waves 0-3 on every SIMD) runs one barrier behind, so on each SIMD one wave
+//   multiplies while the other reads LDS / issues DMA;
+// * the K-tile after next is restaged into the stage just read as soon as the quadrant reads of its
+//   region retired (A rows 0-63 + first col tiles in phase 1, last col tiles in phase 2, A rows 64-127
+//   in phase 3), and one counted vmcnt per K-tile (phase 3) retires the next K-tile; DMA stays in
+//   flight across the raw s_barriers (never __syncthreads(), which would drain it);
+// * XCD-aware bijective block remap + grouped tile order (8 tile-rows) for L2 reuse.
+#include "cs336/kernels.h"
+#include "gemm8.h"
+
+namespace cs336 {
+namespace gemm8 {
+
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int BM = 256, BK = 64, NT = 512;
+constexpr int kGroupM = 8;
+
+__device__ __forceinline__ int xcd_remap(int bid, int total) {
+  const int xcd = bid & 7, q = total >> 3, r = total & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+__device__ __forceinline__ void sbarrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+template <int N>
+__device__ __forceinline__ void vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// sigmoid with the hardware reciprocal (v_exp_f32 + v_rcp_f32): the epilogues run outside the MFMA
+// stream, so every VALU instruction there is on the tile's critical path
+__device__ __forceinline__ float sigmoid_f(float a) { return __builtin_amdgcn_rcpf(1.f + __expf(-a)); }
+
+// Geometry of one instantiation.
+template <int FN>
+struct Geo {
+  static constexpr int BN = 64 * FN;           // tile columns
+  static constexpr int WTN = 16 * FN;          // per-wave columns
+  static constexpr int FB0 = (FN + 1) / 2;     // column tiles of the first column quadrant
+  static constexpr int B0C = 16 * FB0;         // its width
+  static constexpr int A_BYTES = BM * 128;     // [256 rows][64 k] bf16
+  static constexpr int B_BYTES = BN * 128;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  // DMA granules (8 image rows = 1 KiB = one wave instruction) per wave, per restage slice
+  static constexpr int G_A0 = 16 / 8;                 // A rows {0..63, 128..191}: 16 granules
+  static constexpr int G_B0 = (4 * B0C / 8) / 8;      // B rows wc·WTN + [0, B0C)
+  static constexpr int G_B1 = (4 * (WTN - B0C) / 8) / 8;
+  static constexpr int G_A1 = 16 / 8;
+  static constexpr int G_P1 = G_A0 + G_B0, G_P2 = G_B1, G_P3 = G_A1;
+  static constexpr int G_ALL = G_P1 + G_P2 + G_P3;
+  static_assert((4 * B0C / 8) % 8 == 0 && (4 * (WTN - B0C) / 8) % 8 == 0, "B granules must split over 8 waves");
+};
+
+template <int FN, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
+  using G = Geo<FN>;
+  constexpr int BN = G::BN, WTN = G::WTN, FB0 = G::FB0, B0C = G::B0C, STAGE = G::STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // ---- tile coordinates -------------------------------------------------------------------
+  const int tiles_n = p.N / BN;  // EPI 1: N = 2·half, BN/2 units of each half per tile
+  const int tiles_m = p.M / BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = kGroupM * tiles_n;
+  const int first_m = (bid / per_group) * kGroupM;
+  const int gsz = min(tiles_m - first_m, kGroupM);
+  const int tm = first_m + (bid % per_group) % gsz, tn = (bid % per_group) / gsz;
+  const int m0 = tm * BM;
+  // EPI 1: tile column c < BN/2 is W1 row j0 + c, else W3 row half + j0 + c - BN/2
+  const int n0 = tn * (EPI == 1 ? BN / 2 : BN);
+
+  // ---- DMA setup: per wave G_ALL granules; slot order P1 (A0 then B0), P2 (B1), P3 (A1) ------
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.a + (int64_t)m0 * p.lda), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, 0x7fffffff, 0x00020000);
+  uint32_t voff[G::G_ALL];   // per-lane byte offset at k-tile 0
+  uint32_t ldso[G::G_ALL];   // wave-uniform LDS byte offset within a stage
+  {
+    int s = 0;
+    auto a_gran = [&](int row0) {  // A image rows row0..row0+7
+      const int r = row0 + (lane >> 3), lc = (lane & 7) ^ ((r >> 1) & 7);
+      voff[s] = 2u * (uint32_t)(r * p.lda + lc * 8);
+      ldso[s] = (uint32_t)(row0 * 128);
+      ++s;
+    };
+    auto b_gran = [&](int row0) {  // B image rows row0..row0+7 (tile-local column index)
+      const int r = row0 + (lane >> 3), lc = (lane & 7) ^ ((r >> 1) & 7);
+      int grow;
+      if constexpr (EPI == 1) grow = r < BN / 2 ? n0 + r : p.half + n0 + (r - BN / 2);
+      else grow = n0 + r;
+      voff[s] = 2u * (uint32_t)((int64_t)grow * p.ldb + lc * 8);
+      ldso[s] = (uint32_t)(G::A_BYTES + row0 * 128);
+      ++s;
+    };
+#pragma unroll
+    for (int i = 0; i < G::G_A0; ++i) {  // A0 rows: granule g -> rows 8g (g < 8) or 128 + 8(g-8)
+      const int g = wave + 8 * i;
+      a_gran(g < 8 ? 8 * g : 128 + 8 * (g - 8));
+    }
+#pragma unroll
+    for (int i = 0; i < G::G_B0; ++i) {
+      const int g = wave + 8 * i, per = B0C / 8;
+      b_gran((g / per) * WTN + (g % per) * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < G::G_B1; ++i) {
+      const int g = wave + 8 * i, per = (WTN - B0C) / 8;
+      b_gran((g / per) * WTN + B0C + (g % per) * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < G::G_A1; ++i) {
+      const int g = wave + 8 * i;
+      a_gran(g < 8 ? 64 + 8 * g : 192 + 8 * (g - 8));
+    }
+  }
+  auto glds = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t vo, uint32_t so, uint32_t lds_off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(smem + lds_off), 16, vo, so, 0, 0);
+  };
+  // issue slice `part` (1: A0+B0, 2: B1, 3: A1; 0: all) of k-tile kt into stage st
+  auto issue = [&](int part, int kt, int st) {
+    const uint32_t so = (uint32_t)kt * (BK * 2), base = (uint32_t)(st * STAGE);
+    if (part == 0 || part == 1) {
+#pragma unroll
+      for (int i = 0; i < G::G_A0; ++i) glds(ra, voff[i], so, base + ldso[i]);
+#pragma unroll
+      for (int i = G::G_A0; i < G::G_P1; ++i) glds(rb, voff[i], so, base + ldso[i]);
+    }
+    if (part == 0 || part == 2) {
+#pragma unroll
+      for (int i = G::G_P1; i < G::G_P1 + G::G_P2; ++i) glds(rb, voff[i], so, base + ldso[i]);
+    }
+    if (part == 0 || part == 3) {
+#pragma unroll
+      for (int i = G::G_P1 + G::G_P2; i < G::G_ALL; ++i) glds(ra, voff[i], so, base + ldso[i]);
+    }
+  };
+
+  // ---- fragment reads: lane row (l&15), 16-B chunk 4·ks + (l>>4) XOR ((l&15)>>1) -----------
+  const int x = (lane & 15) >> 1, q4 = lane >> 4;
+  const uint32_t lo0 = (uint32_t)((lane & 15) * 128 + ((q4 ^ x) * 16));
+  const uint32_t lo1 = (uint32_t)((lane & 15) * 128 + (((4 + q4) ^ x) * 16));
+  auto frag = [&](uint32_t img_off, int row0, int ks) -> bf16x8 {
+    const char* ptr = smem + img_off + row0 * 128 + (ks ? lo1 : lo0);
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ptr));
+  };
+
+  f32x4 acc[8][FN];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[4][2], fb0[FB0][2], fb1[FN - FB0 > 0 ? FN - FB0 : 1][2];
+  const int arow = wr * 128, bcol = wc * WTN;
+
+  auto mma = [&](int i0, const bf16x8 (&a)[4][2], auto& bq, int j0, int nj) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < nj; ++j)
+          // B fragment as the MFMA's A operand: D = (A·Bᵀ)ᵀ per 16x16 block, so lane l holds
+          // C[m = l&15][n = 4(l>>4) + r] -- four consecutive output columns (one 8/16-B LDS write)
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j][ks], a[i][ks], acc[i0 + i][j0 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nkt = p.K / BK;
+  // ---- prologue: k-tiles 0 and 1 -------------------------------------------------------------
+  issue(0, 0, 0);
+  if (nkt > 1) {
+    issue(0, 1, 1);
+    vmcnt<G::G_ALL>();
+  } else {
+    vmcnt<0>();
+  }
+  sbarrier();
+  if (wr == 1) sbarrier();  // second wave group one barrier behind (SIMD partner staggering)
+
+  for (int t = 0; t < nkt; ++t) {
+    const uint32_t st = (uint32_t)((t & 1) * STAGE);
+    const bool pre = t + 2 < nkt;  // the k-tile after next exists: restage this stage with it
+    // P0: quadrant (rows 0-63, first col tiles)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag(st, arow + 16 * i, ks);
+#pragma unroll
+    for (int j = 0; j < FB0; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag(st + G::A_BYTES, bcol + 16 * j, ks);
+    lgkm0();
+    sbarrier();
+    mma(0, fa, fb0, 0, FB0);
+    sbarrier();
+    // P1: quadrant (rows 0-63, last col tiles); restage A rows 0-63 / B first cols with t+2
+    if constexpr (FN - FB0 > 0) {
+#pragma unroll
+      for (int j = 0; j < FN - FB0; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag(st + G::A_BYTES, bcol + B0C + 16 * j, ks);
+    }
+    if (pre) issue(1, t + 2, t & 1);
+    lgkm0();
+    sbarrier();
+    if constexpr (FN - FB0 > 0) mma(0, fa, fb1, FB0, FN - FB0);
+    sbarrier();
+    // P2: quadrant (rows 64-127, last col tiles); restage B last cols
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag(st, arow + 64 + 16 * i, ks);
+    if (pre) issue(2, t + 2, t & 1);
+    lgkm0();
+    sbarrier();
+    if constexpr (FN - FB0 > 0) mma(4, fa, fb1, FB0, FN - FB0);
+    sbarrier();
+    // P3: quadrant (rows 64-127, first col tiles); retire k-tile t+1, restage A rows 64-127
+    if (t + 1 < nkt) {
+      if (pre) vmcnt<G::G_P1 + G::G_P2>();
+      else vmcnt<0>();
+    }
+    if (pre) issue(3, t + 2, t & 1);
+    sbarrier();
+    mma(4, fa, fb0, 0, FB0);
+    sbarrier();
+  }
+  if (wr == 0) sbarrier();  // balance the stagger
+  lgkm0();
+  sbarrier();
+
+  // ---- epilogue ----------------------------------------------------------------------------
+  // Lane l holds C[m = l&15][n = 4(l>>4) + r] of each 16x16 block (operand-swapped MFMA). Blocks go
+  // through a per-wave LDS scratch [rows][WTN] (8-B bf16 / 16-B fp32 writes), then leave as whole
+  // 16-B row pieces (8 columns) per lane, fully unrolled.
+  constexpr int CPR = WTN / 8;  // 8-column units per scratch row
+  const int m_l = lane & 15, n_l = 4 * (lane >> 4);
+  if constexpr (EPI == 2) {
+    // dh (fp32) in 32-row pieces: scratch 32 × WTN × 4 B per wave (≤ 80 KiB in all)
+    constexpr int PR = 32, UNITS = PR * CPR, PER = UNITS / 64;
+    static_assert(UNITS % 64 == 0, "epilogue units must fill the wave");
+    char* scr = smem + wave * (PR * WTN * 4);
+#pragma unroll
+    for (int piece = 0; piece < 8 / (PR / 16); ++piece) {
+#pragma unroll
+      for (int ib = 0; ib < PR / 16; ++ib)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const f32x4 v = acc[piece * (PR / 16) + ib][j];
+          *reinterpret_cast<f32x4*>(scr + ((16 * ib + m_l) * WTN + 16 * j + n_l) * 4) = v;
+        }
+      __builtin_amdgcn_wave_barrier();
+      // all of this piece's a/b loads first (10 x 16 B per lane in flight), then the math
+      uint4 av[PER], bv[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int q = lane + 64 * u, rr = q / CPR, cc = q % CPR;
+        const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
+        const int col = n0 + bcol + cc * 8;
+        av[u] = *reinterpret_cast<const uint4*>(p.y + row * p.ldy + col);
+        bv[u] = *reinterpret_cast<const uint4*>(p.y + row * p.ldy + p.half + col);
+      }
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int q = lane + 64 * u, rr = q / CPR, cc = q % CPR;
+        const float4 d0 = *reinterpret_cast<const float4*>(scr + (rr * WTN + cc * 8) * 4);
+        const float4 d1 = *reinterpret_cast<const float4*>(scr + (rr * WTN + cc * 8 + 4) * 4);
+        const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
+        const int col = n0 + bcol + cc * 8;
+        const float dh[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+        const bf16_t* ae = reinterpret_cast<const bf16_t*>(&av[u]);
+        const bf16_t* be = reinterpret_cast<const bf16_t*>(&bv[u]);
+        uint4 dav, dbv;
+        bf16_t* da = reinterpret_cast<bf16_t*>(&dav);
+        bf16_t* db = reinterpret_cast<bf16_t*>(&dbv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float a = bf16_to_f32(ae[e]), b = bf16_to_f32(be[e]);
+          const float sg = sigmoid_f(a), gb = dh[e] * sg;
+          da[e] = f32_to_bf16(gb * b * (1.f + a * (1.f - sg)));
+          db[e] = f32_to_bf16(gb * a);
+        }
+        *reinterpret_cast<uint4*>(p.c + row * p.ldc + col) = dav;
+        *reinterpret_cast<uint4*>(p.c + row * p.ldc + p.half + col) = dbv;
+      }
+      __builtin_amdgcn_wave_barrier();
+      lgkm0();  // this piece's scratch reads retired before the next piece's writes
+    }
+  } else {
+    // bf16 in 64-row pieces: scratch 64 × WTN × 2 B per wave (≤ 80 KiB in all)
+    constexpr int PR = 64, UNITS = PR * CPR, PER = UNITS / 64;
+    static_assert(UNITS % 64 == 0, "epilogue units must fill the wave");
+    char* scr = smem + wave * (PR * WTN * 2);
+#pragma unroll
+    for (int piece = 0; piece < 2; ++piece) {
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const f32x4 v = acc[piece * 4 + ib][j];
+          const uint32_t lo = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+          const uint32_t hi = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+          *reinterpret_cast<uint2*>(scr + ((16 * ib + m_l) * WTN + 16 * j + n_l) * 2) = make_uint2(lo, hi);
+        }
+      if constexpr (EPI == 1) {
+        lgkm0();
+        sbarrier();  // the partner wave (wc + 2: the same hidden units' b) wrote its piece
+      } else {
+        __builtin_amdgcn_wave_barrier();
+      }
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int q = lane + 64 * u, rr = q / CPR, cc = q % CPR;
+        const uint4 v = *reinterpret_cast<const uint4*>(scr + (rr * WTN + cc * 8) * 2);
+        const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
+        if constexpr (EPI == 0) {
+          *reinterpret_cast<uint4*>(p.c + row * p.ldc + n0 + bcol + cc * 8) = v;
+        } else {
+          // tile col tc: a side (wc < 2) -> y[:, n0 + tc], b side -> y[:, half + n0 + tc - BN/2]
+          const int tc = bcol + cc * 8;
+          const int ycol = tc < BN / 2 ? n0 + tc : p.half + n0 + (tc - BN / 2);
+          *reinterpret_cast<uint4*>(p.c + row * p.ldc + ycol) = v;
+        }
+      }
+      if constexpr (EPI == 1) {
+        // h = silu(a)·b for this piece, split between the two waves of a pair: the a-side wave
+        // (wc < 2) takes rows 0-31, its b-side partner (wc + 2) rows 32-63
+        constexpr int HU = (PR / 2) * CPR / 64;
+        static_assert(((PR / 2) * CPR) % 64 == 0, "h units must fill the wave");
+        const char* sa = smem + (wc < 2 ? wave : wave - 2) * (PR * WTN * 2);
+        const char* sb = smem + (wc < 2 ? wave + 2 : wave) * (PR * WTN * 2);
+        const int rbase = wc < 2 ? 0 : PR / 2;
+        const int acol0 = (wc & 1) * WTN;  // the pair's a columns within the tile's a half
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+          const int q = lane + 64 * u, rr = rbase + q / CPR, cc = q % CPR;
+          const uint4 va = *reinterpret_cast<const uint4*>(sa + (rr * WTN + cc * 8) * 2);
+          const uint4 vb = *reinterpret_cast<const uint4*>(sb + (rr * WTN + cc * 8) * 2);
+          const bf16_t* ae = reinterpret_cast<const bf16_t*>(&va);
+          const bf16_t* be = reinterpret_cast<const bf16_t*>(&vb);
+          uint4 hv;
+          bf16_t* he = reinterpret_cast<bf16_t*>(&hv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float a = bf16_to_f32(ae[e]);
+            he[e] = f32_to_bf16(a * sigmoid_f(a) * bf16_to_f32(be[e]));
+          }
+          const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
+          *reinterpret_cast<uint4*>(p.h + row * p.ldh + n0 + acol0 + cc * 8) = hv;
+        }
+      }
+      lgkm0();
+      if constexpr (EPI == 1) sbarrier();  // partner reads done before the next piece overwrites
+      else __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+template <int FN, int EPI>
+void launch_t(const Args& p, hipStream_t s) {
+  constexpr int BN = 64 * FN;
+  const int tiles_n = p.N / BN;
+  const dim3 grid((unsigned)((p.M / BM) * tiles_n)), block(NT);
+  hipLaunchKernelGGL((gemm8_kernel<FN, EPI>), grid, block, 0, s, p);
+}
+
+}  // namespace
+
+// Tile width for an output of N columns (EPI 1: N = 2·half): 320 if it divides, else 256, else 0.
+int pick_fn(int N, int epi, int half) {
+  if (epi == 1) {  // a tile holds BN/2 hidden units of each of W1, W3
+    if (half % 160 == 0) return 5;
+    if (half % 128 == 0) return 4;
+    return 0;
+  }
+  if (N % 320 == 0) return 5;
+  if (N % 256 == 0) return 4;
+  return 0;
+}
+
+bool launch(const Args& p, int epi, int fn, hipStream_t s) {
+  if (p.M % BM || p.K % BK || p.K < BK) return false;
+  if (fn == 0) fn = pick_fn(p.N, epi, p.half);
+  if (fn != 4 && fn != 5) return false;
+  if (p.N % (64 * fn)) return false;
+#define CS336_G8(F, E)        \
+  do {                        \
+    launch_t<F, E>(p, s);     \
+    return true;              \
+  } while (0)
+  if (fn == 5) {
+    if (epi == 0) CS336_G8(5, 0);
+    if (epi == 1) CS336_G8(5, 1);
+    if (epi == 2) CS336_G8(5, 2);
+  } else {
+    if (epi == 0) CS336_G8(4, 0);
+    if (epi == 1) CS336_G8(4, 1);
+    if (epi == 2) CS336_G8(4, 2);
+  }
+#undef CS336_G8
+  return false;
+}
+
+}  // namespace gemm8
+}  // namespace cs336

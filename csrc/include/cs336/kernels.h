@@ -37,6 +37,10 @@ void transpose16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int R
 // ---- diagnostics (csrc/ops/occupy.hip): n_workgroups x 256 threads, each holding lds_bytes of LDS,
 // spin for `ms` of wall-clock time, then atomically increment *done
 void occupy(int n_workgroups, int lds_bytes, double ms, int* done, hipStream_t s);
+// co-residency probe: n_workgroups that each wait (up to deadline_ms) until all of them have arrived;
+// state[0] arrivals (reset per launch), state[1] += workgroups that timed out, state[2] = max wait
+// in 100 MHz ticks
+void cohort(int n_workgroups, int lds_bytes, double deadline_ms, int* state, hipStream_t s);
 
 // ---- bf16 MFMA GEMM (csrc/gemm/gemm.hip) ----
 // C[M][N] = Σ_k A(m,k) B(k,n); A(m,k) = a[m·lda+k] (K-major) or a[k·lda+m]; B(k,n) = b[n·ldb+k]

@@ -1,0 +1,49 @@
+"""Turn a ``CS336_GEMM_REPORT`` (bench.py --gemm best, per-problem candidate times) into the
+committed selection table ``cs336_systems/tuning/gemm_table_mi355x.json`` (problem key -> pick).
+
+    CS336_GEMM_TABLE=0 CS336_GEMM_REPORT=gpurun_out/rep.json python bench.py --steps 3 --warmup 2
+    python scripts/gemm_table.py gpurun_out/rep.json [more reports ...]
+
+With several reports (several boxes or runs) each problem takes the candidate with the lowest
+median time over the reports, so one slow box or one noisy timing does not decide it.
+"""
+
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(REPO, "cs336_systems", "tuning", "gemm_table_mi355x.json")
+
+
+def main(paths):
+    times: dict[str, dict[str, list[float]]] = {}
+    for p in paths:
+        for r in json.load(open(p)):
+            for name, ms in r["ms"].items():
+                if isinstance(ms, (int, float)):
+                    times.setdefault(r["key"], {}).setdefault(name, []).append(float(ms))
+    entries, detail = {}, {}
+    for key, cands in times.items():
+        med = {n: statistics.median(v) for n, v in cands.items()}
+        best = min(med, key=med.get)
+        # same 3 % tie rule as the runtime selection: hipBLASLt's default unless clearly beaten
+        pick = best if "blas" not in med or med[best] < 0.97 * med["blas"] else "blas"
+        entries[key] = pick
+        detail[key] = {n: round(v, 4) for n, v in med.items()}
+    # lt pins (hipBLASLt candidate index + kernel name per problem) from the first report that has them
+    pins = []
+    for p in paths:
+        if os.path.exists(p + ".lt.json"):
+            pins = json.load(open(p + ".lt.json"))
+            break
+    doc = {"_meta": {"sources": [os.path.relpath(p, REPO) for p in paths], "rule": "median ms over reports; blas unless beaten by > 3 %",
+                     "median_ms": detail}, "entries": entries, "lt_pins": pins}
+    with open(OUT, "w") as f:
+        json.dump(doc, f, indent=1)
+    print(f"{len(entries)} problems -> {OUT}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -19,7 +19,7 @@ def _run(nproc: int, *extra: str) -> list[dict]:
         sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
         "--master-addr", "127.0.0.1", f"--master-port={find_free_port()}",
         "bench.py", "--gpus", str(nproc), "--steps", "2", "--warmup", "1",
-        "--model", "tiny", "--ctx", "32", "--batch", "2", "--dtype", "fp32", *extra,
+        "--model", "tiny", "--ctx", "32", "--batch", "2", "--dtype", "fp32", "--comm-sweep-mb", "1", "4", *extra,
     ]
     env = dict(os.environ, CS336_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
     out = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
@@ -51,6 +51,33 @@ def test_bench_multirank_json(nproc, extra):
     assert dd["n_buckets"] == len(dd["bucket_sizes_mb"]) >= 1
     assert dd["bucket_mb"]["max"] <= 128.0 + 1e-6
     assert "rccl_version" in dd and isinstance(dd["env"], dict)
+    # the handout's all-reduce table rides in the same line
+    sw = dd["allreduce_sweep_fp32"]
+    assert [r["size_mb"] for r in sw] == [1, 4]
+    for r in sw:
+        assert r["ms"] > 0 and r["algbw_gbs"] > 0
+        assert r["busbw_gbs"] == pytest.approx(r["algbw_gbs"] * 2 * (nproc - 1) / nproc, rel=0.01)
+    assert dd["coresidency_caps"] == {"TENSILE_STREAMK_MAX_CUS": "248", "NCCL_MAX_NCHANNELS": "32"}
     if "--grad-comm-dtype" in extra:
         assert d["config"]["grad_comm_dtype"] == "bf16" and dd["wire_dtype"] == "bfloat16"
         assert dd["wire_mb_total"] == pytest.approx(dd["bucket_mb"]["total"] / 2, rel=0.01)
+
+
+def test_bench_self_launch_without_launcher():
+    """``python bench.py --gpus 2`` with no torchrun and no WORLD_SIZE: bench.py launches the two
+    ranks itself and reports n_gpus 2 (never a mislabeled 1-GPU number)."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--model", "tiny", "--ctx", "32",
+           "--batch", "2", "--dtype", "fp32", "--comm-sweep-mb", "1"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(CS336_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and lines[0]["config"]["parallelism"].startswith("dp2")
+
+
+def test_bench_world_size_mismatch_fails():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", CS336_DIST_BACKEND="gloo")
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--model", "tiny", "--steps", "1"], cwd=REPO, env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 2 and "WORLD_SIZE" in out.stderr

@@ -216,3 +216,31 @@ def _zero_wire_bf16_worker(rank, world):
 @pytest.mark.timeout(120)
 def test_zero_bf16_gradient_wire():
     spawn(_zero_wire_bf16_worker, 2)
+
+
+def test_buckets_survive_zero1_rehome():
+    """a ShardedOptimizer built BEFORE the DDP wrap re-homes every parameter into one
+    flat buffer; bucketing must still split the model (fused groups stay whole)."""
+    from cs336_systems.models import build_model
+    from cs336_systems.parallel.ddp import bucket_params
+
+    torch.manual_seed(0)
+    model = build_model("tiny", 32, vocab_size=128, device=torch.device("cpu"))
+    params = [p for p in model.parameters() if p.requires_grad]
+    before = bucket_params(params, 0.05 * 2**20)
+    flat = torch.empty(sum(p.numel() for p in params))
+    off = 0
+    with torch.no_grad():  # what ZeRO-1's re-home does: one storage for everything, groups contiguous
+        for p in params:
+            v = flat[off: off + p.numel()].view_as(p)
+            v.copy_(p)
+            p.data = v
+            off += p.numel()
+    after = bucket_params(params, 0.05 * 2**20)
+    assert len(after) > 1
+    assert [[id(p) for p in b] for b in after] == [[id(p) for p in b] for b in before]
+    for b in after:  # a fused group never straddles buckets
+        groups = {getattr(p, "_cs336_group", None) for p in b} - {None}
+        for g in groups:
+            members = [p for p in params if getattr(p, "_cs336_group", None) == g]
+            assert all(any(q is p for q in b) for p in members)

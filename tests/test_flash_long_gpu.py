@@ -106,3 +106,23 @@ def test_flash_seq4096_pipelined_forward(monkeypatch, D, causal):
     monkeypatch.setenv("CS336_FA_DMA", "4")
     _run(2, 4, 4096, D, causal, [(0, 0), (1, 3)])
     _run(1, 2, 1000, D, causal, [(0, 0), (0, 1)])
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("D", [64, 80, 128])
+@pytest.mark.parametrize("N", [1100, 1500])
+def test_flash_ragged_long_dma(D, N, causal):
+    """LDS-DMA staging is the default for the backward at Nk >= 1024 and for the causal
+    forward; a ragged Nk (Nk % BN != 0: zero-filled partial last tile) at those lengths, with the
+    native d 80 path included, against the chunked fp32 reference."""
+    _run(1, 2, N, D, causal, [(0, 0), (0, 1)])
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("D", [64, 128])
+def test_flash_dma_forced_short_ragged(monkeypatch, D, causal):
+    """CS336_FA_DMA=2 (LDS-DMA forward AND backward) on short, ragged inputs, below the lengths where
+    the default would choose it."""
+    monkeypatch.setenv("CS336_FA_DMA", "2")
+    _run(1, 2, 200, D, causal, [(0, 0), (0, 1)])
+    _run(2, 1, 77, D, causal, [(0, 0), (1, 0)])

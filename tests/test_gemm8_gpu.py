@@ -1,0 +1,95 @@
+"""gemm8 (csrc/gemm/gemm8.hip): the NT projection GEMM with fused SwiGLU epilogues, against an fp32
+PyTorch reference of the same op (bf16 inputs, fp32 math, bf16-rounded where the kernel rounds)."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cs():
+    from cs336_systems import ops
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    assert ops.load_ext(), ops.load_error()
+    return torch.ops.cs336
+
+
+def _rand(*s, scale=1.0, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return ((torch.rand(*s, device="cuda", generator=g) * 2 - 1) * scale).to(torch.bfloat16)
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("M,N,K,fn", [(256, 320, 64, 0), (512, 640, 192, 5), (256, 512, 128, 4), (768, 1600, 1600, 0),
+                                      (512, 1280, 320, 4), (256, 256, 4096, 0)])
+def test_gemm8_plain(M, N, K, fn):
+    cs = _cs()
+    a, b = _rand(M, K, seed=1), _rand(N, K, seed=2)
+    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    cs.gemm8(a, b, c, 0, fn, None, None, 0)
+    ref = a.float() @ b.float().t()
+    assert _rel(c, ref) < 5e-3
+    # exact tile placement: bf16 rounding of the fp32 sum, element by element
+    torch.testing.assert_close(c.float(), ref.to(torch.bfloat16).float(), rtol=2e-2, atol=2e-2 * ref.abs().max().item() / 50)
+
+
+def test_gemm8_strided_operands():
+    """Row strides wider than K (views into wider buffers), as the fused QKV / Wᵀ layouts produce."""
+    cs = _cs()
+    M, N, K = 512, 640, 128
+    abuf, bbuf = _rand(M, K + 64, seed=3), _rand(N, K + 192, seed=4)
+    a, b = abuf[:, 32:32 + K], bbuf[:, :K]
+    cbuf = torch.zeros(M, N + 64, device="cuda", dtype=torch.bfloat16)
+    c = cbuf[:, 64:]
+    cs.gemm8(a, b, c, 0, 0, None, None, 0)
+    assert _rel(c, a.float() @ b.float().t()) < 5e-3
+    assert torch.count_nonzero(cbuf[:, :64]) == 0
+
+
+@pytest.mark.parametrize("half,fn", [(320, 5), (640, 0), (256, 4), (6400, 5)])
+def test_gemm8_swiglu_forward(half, fn):
+    cs = _cs()
+    M, K = 512, 1600 if half == 6400 else 192
+    x, w13 = _rand(M, K, seed=5), _rand(2 * half, K, scale=0.1, seed=6)
+    y = torch.empty(M, 2 * half, device="cuda", dtype=torch.bfloat16)
+    h = torch.empty(M, half, device="cuda", dtype=torch.bfloat16)
+    cs.gemm8(x, w13, y, 1, fn, h, None, half)
+    yr = x.float() @ w13.float().t()
+    assert _rel(y, yr) < 5e-3
+    yb = y.float()  # h is computed from the stored (bf16) a and b
+    hr = torch.nn.functional.silu(yb[:, :half]) * yb[:, half:]
+    assert _rel(h, hr) < 5e-3
+
+
+@pytest.mark.parametrize("half,fn", [(320, 5), (640, 0), (256, 4), (6400, 5)])
+def test_gemm8_swiglu_backward(half, fn):
+    cs = _cs()
+    M, K = 512, 1600 if half == 6400 else 192
+    dy, w2t = _rand(M, K, seed=7), _rand(half, K, scale=0.1, seed=8)  # w2t = W2ᵀ (half, d_model)
+    y = _rand(M, 2 * half, scale=3.0, seed=9)
+    dab = torch.empty(M, 2 * half, device="cuda", dtype=torch.bfloat16)
+    cs.gemm8(dy, w2t, dab, 2, fn, None, y, half)
+    dh = dy.float() @ w2t.float().t()
+    a, b = y.float()[:, :half], y.float()[:, half:]
+    s = torch.sigmoid(a)
+    da = dh * b * s * (1 + a * (1 - s))
+    db = dh * a * s
+    assert _rel(dab[:, :half], da) < 5e-3
+    assert _rel(dab[:, half:], db) < 5e-3
+
+
+def test_gemm8_xl_shapes():
+    """The production shapes of the XL step (24576 tokens): QKV and W2 forward, W1|W3 input grad."""
+    cs = _cs()
+    M = 24576
+    for N, K in ((4800, 1600), (1600, 6400), (1600, 12800)):
+        a, b = _rand(M, K, seed=N), _rand(N, K, scale=0.05, seed=K)
+        c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        cs.gemm8(a, b, c, 0, 0, None, None, 0)
+        ref = torch.mm(a, b.t())  # hipBLASLt bf16 (fp32 accumulate)
+        assert _rel(c, ref) < 5e-3, (N, K)
