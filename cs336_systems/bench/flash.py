@@ -81,8 +81,15 @@ def leaderboard(compile_fn: bool = True) -> dict:
         loss = o.sum()
         loss.backward()
 
-    ms = do_bench(fb, warmup=1000, rep=10000, flush_cache=False)[0]
-    return dict(config="leaderboard (16,16384,64) bf16 causal fwd+bwd", ms=ms, tflops=attn_flops(16, 1, 16384, 64, True, "fwd_bwd") / (ms * 1e-3) / 1e12, compiled=compile_fn)
+    # cold caches every repetition, as triton.testing.do_bench does (it zeroes a cache-sized buffer
+    # before each call): q/k/v (~100 MB) would otherwise sit in the 256 MB Infinity Cache. The
+    # handout's warmup=1000 / rep=10000 are Triton's time budgets in ms; here they are counts,
+    # 100 warmup calls and 2000 timed ones (~5 s of timing at ~2.5 ms per call)
+    ms = do_bench(fb, warmup=100, rep=2000, flush_cache=True)[0]
+    warm = do_bench(fb, warmup=10, rep=200, flush_cache=False)[0]
+    return dict(config="leaderboard (16,16384,64) bf16 causal fwd+bwd", ms=ms,
+                tflops=attn_flops(16, 1, 16384, 64, True, "fwd_bwd") / (ms * 1e-3) / 1e12, compiled=compile_fn,
+                protocol="do_bench, L2 + Infinity Cache flushed before every call (512 MiB write)", warm_cache_ms=warm)
 
 
 def main(argv=None):

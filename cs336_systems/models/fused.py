@@ -202,6 +202,36 @@ def refresh_bf16_shadows(params, transposed: bool = False) -> None:
             mark_shadow_t_synced(p)
 
 
+@torch.no_grad()
+def refresh_transposed(params) -> int:
+    """Re-write the Wᵀ shadows of ``params`` from their current bf16 shadows -- one transpose per run
+    of row-adjacent weights that share one Wᵀ tensor (a fused QKV / W1|W3 group is one launch) --
+    and mark them in sync. For weights whose shadow was refreshed outside the fused AdamW (ZeRO
+    parameter gathers), so the next forward finds a valid Wᵀ instead of transposing each weight.
+    Returns the number of transposes launched."""
+    runs: dict[tuple, list] = {}
+    for p in params:
+        wt = get_shadow_t(p)
+        if wt is None or not shadow_valid(p):
+            continue
+        runs.setdefault((wt.untyped_storage().data_ptr(), wt.shape[0]), []).append(p)
+    n = 0
+    for ps in runs.values():
+        ps.sort(key=lambda t: get_shadow_t(t).storage_offset())
+        src = _adjacent_rows([get_shadow(p) for p in ps])
+        dst = _adjacent_cols([get_shadow_t(p) for p in ps])
+        if src is not None and dst is not None and src.is_cuda and ops.ext_available() and src.shape[0] % 8 == 0:
+            _hip().transpose2d_into(src, dst)
+            n += 1
+        else:
+            for p in ps:
+                get_shadow_t(p).copy_(get_shadow(p).t())
+                n += 1
+        for p in ps:
+            mark_shadow_t_synced(p)
+    return n
+
+
 def _adjacent_cols(ts: list[torch.Tensor]) -> torch.Tensor | None:
     """If ``ts`` are column-adjacent blocks (unit column stride) of one storage, the combined view."""
     t0 = ts[0]
@@ -425,7 +455,11 @@ class FusedLinearFn(torch.autograd.Function):
             and xt_given.shape == (x2.shape[1], x2.shape[0])
             and xt_given.stride(1) == 1
         )
-        ctx.xt = x2.is_cuda and any(ctx.needs_input_grad[1:]) and (
+        # weight gradient by gemm8w straight from token-major X and dY: save X as is, no Xᵀ / dYᵀ
+        ctx.dw_g8w = (any(ctx.needs_input_grad[1:]) and x2.is_cuda and x2.dtype == torch.bfloat16
+                      and gemm.dw_g8w_enabled() and gemm._aligned_rows(x2) and x2.shape[0] % 64 == 0
+                      and gemm._dw_plan(x2.shape[0], w.shape[0], x2.shape[1]) is not None)
+        ctx.xt = x2.is_cuda and any(ctx.needs_input_grad[1:]) and not ctx.dw_g8w and (
             use_given or _save_transposed(x2.shape[1], w.shape[0]))
         # The input-gradient GEMM dY·W reads W k-strided; from a transposed copy Wᵀ both operands
         # are K-major, which hipBLASLt runs 1.15-1.4x faster (profiles/r1_gemm_dw_layouts.json).
@@ -504,11 +538,16 @@ class FusedLinearFn(torch.autograd.Function):
                 and gemm.dw_concurrent_ok(dy2, x2, ctx.xt)  # never a stream-K GEMM beside another GEMM
             )
             dyt = None
-            if not side and dy2.is_cuda and dy2.dtype == torch.bfloat16 and _dy_transposed(ctx.x_shape[-1], dy2.shape[1]):
+            g8w = getattr(ctx, "dw_g8w", False) and not side and gemm.dw_g8w_ok(dy2, x2)
+            if g8w:
+                take_transposed_grad(dy2)  # drop a producer's dYᵀ offer: not needed
+            elif not side and dy2.is_cuda and dy2.dtype == torch.bfloat16 and _dy_transposed(ctx.x_shape[-1], dy2.shape[1]):
                 dyt = take_transposed_grad(dy2)
                 if dyt is None:
                     dyt = _transpose(dy2)
-            if dyt is not None:  # dYᵀ (N_out, tokens); x2 is X or Xᵀ
+            if g8w:  # token-major dY and X, fp32 dW (straight into the DDP bucket when there is one)
+                dw_fn = lambda out=None, cs=False: gemm.mm_dw(dy2, x2, out=out)  # noqa: E731
+            elif dyt is not None:  # dYᵀ (N_out, tokens); x2 is X or Xᵀ
                 dw_fn = lambda out=None, cs=False: gemm.mm_dyt_fp32(dyt, x2, ctx.xt, out=out)  # noqa: E731
             elif ctx.xt:  # x2 holds Xᵀ (K_in, tokens)
                 dw_fn = lambda out=None, cs=False: gemm.mm_tn_fp32_xt(dy2, x2, out=out, concurrent_safe=cs)  # noqa: E731

@@ -393,3 +393,79 @@ def mm_tn_fp32(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = Non
     impls = {"blas": blas, "lt": lt, "cs336": cs, **extra}
     r = impls[_select("tn32", dy, x, out, blas, lt, cs, dw=True, extra=extra)]()
     return out if out is not None else r
+
+
+# ------------------------------------------------------------------------------------------
+# weight gradients straight from token-major operands (csrc/gemm/gemm8w.hip)
+# ------------------------------------------------------------------------------------------
+def dw_g8w_enabled() -> bool:
+    """``CS336_DW=g8w`` (default): projection weight gradients dW = dYᵀ·X run the cs336 gemm8w kernel
+    on the token-major dY and X -- no dYᵀ / Xᵀ transposes in forward or backward; ``CS336_DW=blas``
+    restores the hipBLASLt paths (best-mode table, Xᵀ / dYᵀ layouts)."""
+    return os.environ.get("CS336_DW", "g8w") == "g8w" and ext_available()
+
+
+# measured picks (scripts/gemm8w_bench.py, profiles/r3_gemm8w_bench.json): (tokens, N_out, K_in) ->
+# (transposed roles, split-K count)
+DW_PLANS: dict = {
+    # XL (d 1600, d_ff 6400) at 24576 tokens, profiles/r3_gemm8w_bench.json (ms, vs hipBLASLt):
+    (24576, 12800, 1600): (False, 1),  # W1|W3: 0.835 (default 1.27, lt 1.23, Xᵀ-layout blas 0.88)
+    (24576, 1600, 6400): (True, 2),  # W2: 0.442 (lt 0.60; from dYᵀ 0.43 + its transpose)
+    (24576, 4800, 1600): (False, 5),  # QKV: 0.377 (default 0.386)
+    (24576, 1600, 1600): (False, 7),  # O: 0.139 (lt 0.224; split-K torch 0.164 + dYᵀ transpose)
+}
+
+
+def _dw_plan(T: int, n_out: int, k_in: int) -> tuple[bool, int] | None:
+    """(transposed roles, split count) for dW [n_out, k_in] over T tokens: the measured plan, else a
+    cost model -- padded row tiles of 256, column tiles of 320/256, quantisation over the 256 CUs,
+    split-K slab traffic."""
+    hit = DW_PLANS.get((T, n_out, k_in))
+    if hit is not None:
+        return hit
+    best, best_t = None, float("inf")
+    for trans in (False, True):
+        M, N = (k_in, n_out) if trans else (n_out, k_in)
+        bn = 320 if N % 320 == 0 else (256 if N % 256 == 0 else 0)
+        if not bn or M % 8:
+            continue
+        tiles = -(-M // 256) * (N // bn)
+        for sk in (1, 2, 3, 4, 5, 6, 7, 8):
+            if T % 64 or (T // 64) < 4 * sk:
+                continue
+            wgs = tiles * sk
+            eff = wgs / (-(-wgs // 256) * 256)
+            t = 2.0 * T * (-(-M // 256) * 256) * N / (eff * 1.35e15)
+            if sk > 1:
+                t += (sk + 2) * M * N * 4 / 5.0e12
+            if t < best_t:
+                best, best_t = (trans, sk), t
+    return best
+
+
+def dw_g8w_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    return (dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.dim() == 2 and x.dim() == 2
+            and dy.shape[0] == x.shape[0] and _aligned_rows(dy) and _aligned_rows(x) and dy.shape[0] % 64 == 0
+            and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0 and _dw_plan(dy.shape[0], dy.shape[1], x.shape[1]) is not None)
+
+
+def mm_dw(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
+    """``dy.T @ x`` with an fp32 result from token-major ``dy`` (T, N_out) and ``x`` (T, K_in) --
+    written into ``out`` (e.g. a DDP bucket view; ``accumulate``: added to it) when given."""
+    T, n_out, k_in = dy.shape[0], dy.shape[1], x.shape[1]
+    trans, sk = _dw_plan(T, n_out, k_in)
+    a, b = (x, dy) if trans else (dy, x)
+    if out is None:
+        out = torch.empty(n_out, k_in, device=dy.device, dtype=torch.float32)
+        accumulate = False
+    direct = sk == 1 and out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0
+    if direct:
+        ops().gemm8w(a, b, out, 1, trans, accumulate, 0)
+        return out
+    slabs = torch.empty(sk, n_out, k_in, device=dy.device, dtype=torch.float32)
+    ops().gemm8w(a, b, slabs, sk, trans, False, 0)
+    if accumulate:
+        out.add_(slabs.sum(0))
+    else:
+        torch.sum(slabs, dim=0, out=out)
+    return out

@@ -206,11 +206,15 @@ class ShardedOptimizer(torch.optim.Optimizer):
     def _after_gather(self, f: dict) -> None:
         if not self._shadows:
             return
-        # .data copies do not bump p._version: re-cast the received parameters' shadows explicitly
-        from ..models.fused import refresh_bf16_shadows
+        # .data copies do not bump p._version: re-cast the received parameters' shadows explicitly,
+        # then re-write their Wᵀ shadows (one transpose per fused group / weight run), so the next
+        # forward uses Wᵀ for every weight instead of transposing the (W-1)/W it does not own
+        from ..models.fused import refresh_bf16_shadows, refresh_transposed
 
         mine = {id(p) for p in f["mine"]}
-        refresh_bf16_shadows([p for p in f["params"] if id(p) not in mine])
+        received = [p for p in f["params"] if id(p) not in mine]
+        refresh_bf16_shadows(received)
+        refresh_transposed(received)
 
     # ------------------------------------------------------------------------------------------
     def state_dict(self):

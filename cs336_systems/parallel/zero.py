@@ -33,7 +33,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ..models.fused import _SHADOW, dw_stream_for, mark_shadow_synced, sync_dw_stream
+from ..models.fused import _SHADOW, _attach_transposed, _transpose_weight, dw_stream_for, mark_shadow_synced, refresh_transposed, sync_dw_stream
 from ..ops.adamw import FusedAdamW, multi_tensor_l2norm
 from ..utils.profiling import annotate
 from .comm import broadcast_module_, supports_avg
@@ -161,6 +161,10 @@ class ZeroDDP(nn.Module):
                     if sbuf is not None and p.dim() == 2:
                         setattr(p, _SHADOW, sbuf[off : off + k].view_as(p))
                     off += k
+                if sbuf is not None and _transpose_weight():
+                    # Wᵀ shadows (K-major operand of the input-gradient GEMM), re-written from the
+                    # gathered bf16 shadows once per step (refresh_transposed: one launch per run)
+                    _attach_transposed([p for p in ps if p.dim() == 2])
                 master = nn.Parameter(pbuf[r * shard : (r + 1) * shard])
                 # one rank: the "shard" is the whole bucket, no collective runs and the update
                 # kernel writes the bf16 shadows itself (as FusedAdamW does without ZeRO)
@@ -314,6 +318,8 @@ class ZeroDDP(nn.Module):
                 for p in b.params:
                     if b.sbuf is not None and p.dim() == 2:
                         mark_shadow_synced(p)
+                if b.sbuf is not None:
+                    refresh_transposed(b.params)
             return
         for b in reversed(self.buckets):  # forward order: the last buckets hold the first layers
             with annotate(f"comm.ag{b.idx}"):
@@ -360,12 +366,17 @@ class ZeroDDP(nn.Module):
         if b.bf16:  # the gathered bytes ARE the shadows
             for p in b.params:
                 mark_shadow_synced(p)
+            refresh_transposed(b.params)
         elif b.sbuf is not None:
             self._refresh_shadows(b)
 
     def _wait_buckets(self, ids) -> None:
         for i in ids:
             self._wait_bucket(self.buckets[i])
+        # a forward that reads the fp32 masters (no bf16 autocast: the shadows are not used) must
+        # not see other ranks' stale masters after a bf16-only gather
+        if self._masters_stale and not (torch.is_autocast_enabled("cuda") or torch.is_autocast_enabled("cpu")):
+            self._gather_masters()
 
     def _wait_all_gathers(self) -> None:
         for b in reversed(self.buckets):
@@ -377,6 +388,7 @@ class ZeroDDP(nn.Module):
         for p in b.params:
             if p.dim() == 2:
                 mark_shadow_synced(p)
+        refresh_transposed(b.params)
 
     def wait_for_params(self) -> None:
         """Make the current stream wait for every pending parameter all-gather and bring every fp32

@@ -398,6 +398,22 @@ at::Tensor transpose2d(const at::Tensor& x) {
   return out;
 }
 
+// out = x.T into an existing (possibly column-block) view: out (C, R) with unit column stride
+void transpose2d_into(const at::Tensor& x, at::Tensor& out) {
+  check_cuda(x, "x");
+  check_cuda(out, "out");
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.stride(1) == 1 && out.stride(1) == 1 && x.element_size() == 2 &&
+                  out.scalar_type() == x.scalar_type(),
+              "cs336: transpose2d_into needs 2-D 16-bit row-major tensors of one dtype");
+  TORCH_CHECK(out.size(0) == x.size(1) && out.size(1) == x.size(0), "cs336: transpose2d_into shape");
+  TORCH_CHECK(x.size(0) % 8 == 0 && x.size(1) % 8 == 0 && x.stride(0) % 8 == 0 && out.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "cs336: transpose2d_into needs dims/strides multiples of 8 and 16-B aligned bases");
+  c10::DeviceGuard g(x.device());
+  if (x.numel() == 0) return;
+  cs336::transpose16(x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0), (int)x.size(0), (int)x.size(1), stream());
+}
+
 static bool f32_or_bf16(const at::Tensor& t) {
   return t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16;
 }
@@ -836,6 +852,52 @@ void gemm8(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, int64_t epi,
   TORCH_CHECK(cs336::gemm8::launch(p, (int)epi, (int)fn, stream()), "cs336: gemm8 launch (fn ", fn, ")");
 }
 
+// Weight gradient straight from token-major operands (csrc/gemm/gemm8w.hip):
+//   out[m][n] (+)= Σ_t a[t][m]·b[t][n]    (trans_out: out[n][m])
+// a (K, M) and b (K, N) bf16 with unit column stride; out fp32 (M, N) or (N, M) with unit column
+// stride; splits > 1: out is (splits, rows, cols) dense slabs, one partial per split.
+void gemm8w(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, int64_t splits, bool trans_out,
+            bool accumulate, int64_t fn) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
+                  a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1,
+              "cs336: gemm8w needs row-major bf16 CUDA operands");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K, "cs336: gemm8w contraction mismatch");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0 && M % 8 == 0 && N % 8 == 0,
+              "cs336: gemm8w needs 16-B aligned rows");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat, "cs336: gemm8w out must be fp32 CUDA");
+  const int64_t rows = trans_out ? N : M, cols = trans_out ? M : N;
+  if (splits > 1) {
+    TORCH_CHECK(out.dim() == 3 && out.size(0) == splits && out.size(1) == rows && out.size(2) == cols &&
+                    out.is_contiguous() && !accumulate,
+                "cs336: gemm8w split-K out must be contiguous (splits, rows, cols) slabs");
+  } else {
+    TORCH_CHECK(out.dim() == 2 && out.size(0) == rows && out.size(1) == cols && out.stride(1) == 1 &&
+                    out.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+                "cs336: gemm8w out shape/alignment");
+  }
+  cs336::gemm8::WArgs p{};
+  p.a = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  p.b = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  p.c = out.data_ptr<float>();
+  p.lda = a.stride(0);
+  p.ldb = b.stride(0);
+  p.ldc = splits > 1 ? cols : out.stride(0);
+  p.slab_stride = splits > 1 ? rows * cols : 0;
+  p.a_elems = (K - 1) * a.stride(0) + M;
+  p.b_elems = (K - 1) * b.stride(0) + N;
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.splits = (int)splits;
+  p.trans_out = trans_out ? 1 : 0;
+  p.accumulate = accumulate ? 1 : 0;
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(cs336::gemm8::launch_w(p, (int)fn, stream()), "cs336: gemm8w does not take M=", M, " N=", N, " K=", K,
+              " splits=", splits);
+}
+
 TORCH_LIBRARY(cs336, m) {
   m.def(
       "fa_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None, "
@@ -848,6 +910,7 @@ TORCH_LIBRARY(cs336, m) {
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
   m.def("add_rmsnorm_fwd(Tensor x, Tensor r, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor, Tensor)");
   m.def("transpose2d(Tensor x) -> Tensor");
+  m.def("transpose2d_into(Tensor x, Tensor(a!) out) -> ()");
   m.def("gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, ScalarType out_dtype, int bm=0, int bn=0, int splits=0) -> Tensor");
   m.def("gemm_out(Tensor a, Tensor b, bool trans_a, bool trans_b, Tensor(a!) out, bool accumulate=False, int bm=0, int bn=0, int splits=0) -> ()");
   m.def("gemm_ok(Tensor a, Tensor b, bool trans_a, bool trans_b) -> bool", &gemm_ok);
@@ -880,6 +943,7 @@ TORCH_LIBRARY(cs336, m) {
   m.def("cohort(int n_workgroups, int lds_bytes, float deadline_ms, Tensor(a!) state) -> ()");
   m.def("gemm8(Tensor a, Tensor b, Tensor(a!) c, int epi, int fn, Tensor(b!)? h, Tensor? y, int half) -> ()");
   m.def("gemm8_ok(int M, int N, int K, int epi, int half) -> bool", &gemm8_ok);
+  m.def("gemm8w(Tensor a, Tensor b, Tensor(a!) out, int splits, bool trans_out, bool accumulate, int fn) -> ()");
   m.def("multi_tensor_scale_(Tensor(a!)[] tensors, Tensor scale) -> ()");
 }
 
@@ -890,6 +954,7 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
   m.impl("transpose2d", &transpose2d);
+  m.impl("transpose2d_into", &transpose2d_into);
   m.impl("gemm", &gemm_new);
   m.impl("gemm_out", &gemm_out);
   m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
@@ -911,5 +976,6 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("occupy", &occupy);
   m.impl("cohort", &cohort);
   m.impl("gemm8", &gemm8);
+  m.impl("gemm8w", &gemm8w);
   m.impl("multi_tensor_scale_", &multi_tensor_scale_);
 }

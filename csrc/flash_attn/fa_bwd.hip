@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
     auto dstep = [&](int j, auto slot) __attribute__((always_inline)) {
       if (NS == 3 && j + 1 < ntiles) wait_vmcnt<2 * Dma::PER_WAVE>();
       else wait_vmcnt<0>();
-      __syncthreads();
+      dma_barrier();
       if (j + NS - 1 < ntiles) issue(j + NS - 1);
       const int B = slot;  // integral_constant (unrolled loop) or runtime slot
       tile(j, smem + B * 2 * TILE);
@@ -585,8 +585,8 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
       // every wave loads the same L / delta rows (identical bytes): uniform vmcnt accounting
       const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)(Lp + it * BQ), (short)0, rows * 4, 0x00020000);
       const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(Dp + it * BQ), (short)0, rows * 4, 0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (__attribute__((address_space(3))) void*)(base + 2 * TILE), 16, row_off, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (__attribute__((address_space(3))) void*)(base + 2 * TILE + 1024), 16, row_off, 0, 0, 0);
+      dma16(rl, lds_addr(base + 2 * TILE), row_off, 0);
+      dma16(rd, lds_addr(base + 2 * TILE + 1024), row_off, 0);
     };
     constexpr int PER_TILE = 2 * Dma::PER_WAVE + 2;
 #pragma unroll
@@ -595,7 +595,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
     auto dstep = [&](int it, auto slot, auto mask_tag) __attribute__((always_inline)) {
       if (NS == 3 && it + 1 < qt_end) wait_vmcnt<PER_TILE>();
       else wait_vmcnt<0>();
-      __syncthreads();
+      dma_barrier();
       if (it + NS - 1 < qt_end) issue(it + NS - 1);
       const int B = slot;  // integral_constant (unrolled loop) or runtime slot
       tile(it, smem + B * SLOT, mask_tag);

@@ -268,6 +268,22 @@ __device__ __forceinline__ void rope_inv4(float& v0, float& v1, float& v2, float
 // valid count and the zero padding chunks of d_head 80 (chunk >= CREAL) read out of the buffer
 // descriptor's range; the kernel zero-fills its LDS ring once at entry, so such slots hold zeros or
 // finite stale rows, which the masks turn into exact zeros (P = 0 for keys >= Nk / queries >= Nq).
+// One LDS-DMA wave instruction (buffer_load_dwordx4 ... lds: 64 lanes x 16 B into 1 KB of LDS at
+// the wave-uniform address lds_addr) in inline asm. Issued through the builtin, the load is a pending
+// LDS write that hipcc's waitcnt pass cannot disambiguate from the kernel's LDS reads, so it put
+// s_waitcnt vmcnt(0) in front of the first read after every issue -- draining the prefetch ring at
+// each tile. Every DMA of these kernels goes through here (M0 is written by no other code in them);
+// its data is waited for by the explicit counted wait_vmcnt + dma_barrier before any read.
+__device__ __forceinline__ void dma16(const __amdgpu_buffer_rsrc_t& rs, uint32_t lds_addr, uint32_t voff, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen lds"
+               :
+               : "v"(voff), "s"(lds_addr), "s"(rs), "s"(soff)
+               : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
+}
+
 template <int ROWS, int RB, int CREAL, int ES>
 struct TileDma {
   static constexpr int CPR = RB / 16;
@@ -287,16 +303,27 @@ struct TileDma {
   __device__ __forceinline__ void issue(const void* tile, int rows_valid, int64_t ld, char* img, int wave) const {
     const uint32_t bytes = rows_valid > 0 ? (uint32_t)((int64_t)(rows_valid - 1) * ld * ES + CREAL * 16) : 0u;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)tile, (short)0, (int)bytes, 0x00020000);
+    const uint32_t base = lds_addr(img);
 #pragma unroll
-    for (int i = 0; i < PER_WAVE; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(img + 1024 * (i * 4 + wave)),
-                                               16, voff[i], 0, 0, 0);
+    for (int i = 0; i < PER_WAVE; ++i) dma16(rsrc, base + 1024 * (i * 4 + wave), voff[i], 0);
   }
 };
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Workgroup barrier that keeps LDS-DMA in flight: __syncthreads()'s fence makes hipcc emit
+// s_waitcnt vmcnt(0) in front of the s_barrier, and an LDS-DMA is a pending write on the VM counter,
+// so it drained the whole prefetch ring at every tile (the counted wait_vmcnt before it did nothing).
+// Here: this wave's LDS reads/writes retired (lgkmcnt(0): the WAR/RAW for other waves), then a raw
+// s_barrier the compiler cannot move anything across.
+__device__ __forceinline__ void dma_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // zero a block of LDS (all 256 threads; bytes % 4096 == 0)

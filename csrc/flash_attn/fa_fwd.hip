@@ -267,20 +267,20 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
     }
     issue_k(NS - 1);
     wait_vmcnt<(2 * NS - 2) * PW>();  // K(0) landed
-    __syncthreads();
+    dma_barrier();
     f32x16 sa[2], sb[2];
     if (active(0)) s_tile(Kr, sa);
     // one iteration: publish K(j+1), V(j); refill; finish tile j with S^T(j+1) inside its softmax
     auto body = [&](int j, f32x16 (&cur)[2], f32x16 (&nxt)[2]) {
       wait_vmcnt<(2 * NS - 4) * PW>();
-      __syncthreads();
+      dma_barrier();
       issue_v(j + NS - 1);
       issue_k(j + NS);
       if (active(j)) finish(j, Vr + (j % NS) * TILE, cur, [&] { s_tile(Kr + ((j + 1) % NS) * TILE, nxt); });
     };
     auto last = [&](int j, f32x16 (&cur)[2]) {
       wait_vmcnt<0>();  // V(j) (and the trailing empty groups)
-      __syncthreads();
+      dma_barrier();
       if (active(j)) finish(j, Vr + (j % NS) * TILE, cur, [] {});
     };
     int j = 0;
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
       // the barrier then publishes every wave's pieces and retires all reads of tile j-1's slot
       if (NS == 3 && j + 1 < ntiles) wait_vmcnt<2 * Dma::PER_WAVE>();
       else wait_vmcnt<0>();
-      __syncthreads();
+      dma_barrier();
       if (j + NS - 1 < ntiles) issue(j + NS - 1);
       const int B = slot;  // integral_constant (unrolled loop) or runtime slot
       tile(j, smem + B * 2 * TILE);

@@ -28,5 +28,22 @@ struct Args {
 int pick_fn(int N, int epi, int half);
 bool launch(const Args& p, int epi, int fn, hipStream_t s);
 
+// Weight gradient with both operands MN-major (csrc/gemm/gemm8w.hip): C[m][n] = Σ_t A[t][m]·B[t][n],
+// A [K][lda] (m < M), B [K][ldb] (n < N), fp32 out. trans_out: C[m][n] stored at c[n·ldc + m].
+// splits > 1: split s writes its partial to c + s·slab_stride (dense slabs, reduced by the caller).
+// accumulate: c += (splits == 1 only). Requires K % 64 == 0, N % (64·fn) == 0 (fn 5 or 4), M % 4 == 0;
+// M is padded to the 256-row tile (rows >= M are computed and dropped).
+struct WArgs {
+  const uint16_t* a;
+  const uint16_t* b;
+  float* c;
+  int64_t lda, ldb, ldc, slab_stride;
+  int64_t a_elems, b_elems;  // storage extent of a / b from their base pointers (bounds for the DMA)
+  int M, N, K;
+  int splits;
+  int trans_out, accumulate;
+};
+bool launch_w(const WArgs& p, int fn, hipStream_t s);
+
 }  // namespace gemm8
 }  // namespace cs336

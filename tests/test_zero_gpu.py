@@ -88,3 +88,50 @@ def test_zero_bench_two_ranks_one_gpu():
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2+zero2"
     assert out["final_loss"] == out["final_loss"] and out["final_loss"] < 20  # finite, trained
+
+
+def _step(model, opt, z, x):
+    opt.zero_grad(set_to_none=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = ops.cross_entropy(model(x), x)
+    loss.backward()
+    if z is not None:
+        z.finish_gradient_synchronization()
+    opt.step()
+
+
+@pytest.mark.parametrize("gather", ["fp32", "bf16"])
+def test_zero_gather_keeps_wt_shadows(rccl_world1, gather):
+    """after the parameter all-gather the Wᵀ shadows are re-written (one transpose
+    per fused group), so the forward uses Wᵀ for every projection instead of transposing."""
+    from cs336_systems.models.fused import get_shadow_t, shadow_t_valid
+
+    zero = ZeroDDP(_lm(), bucket_size_mb=2.0, bf16_shadows=True, gather_dtype=gather, _collectives_at_world1=True, **OPT)
+    x = torch.randint(0, 512, (4, 128), device=DEV, generator=torch.Generator(DEV).manual_seed(0))
+    _step(zero, zero.optimizer, zero, x)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        zero(x)  # forward pre-hooks wait for the gathers and refresh shadows + Wᵀ
+    n = 0
+    for name, p in zero.module.named_parameters():
+        if p.dim() == 2 and get_shadow_t(p) is not None:
+            assert shadow_t_valid(p), name
+            assert torch.equal(get_shadow_t(p), get_shadow(p).t()), name
+            n += 1
+    assert n >= 4 * 2  # q/k/v/o/w1/w2/w3 of both layers (+ lm head)
+
+
+def test_zero_fp32_forward_after_bf16_gather(rccl_world1):
+    """with gather_dtype='auto'/'bf16' only the bf16 shadows travel; a forward that reads
+    the fp32 masters (no autocast) must gather them first, and match the unsharded model."""
+    ref = _lm()
+    ref_opt = ops.FusedAdamW(ref.parameters(), bf16_shadows=True, **OPT)
+    zero = ZeroDDP(_lm(), bucket_size_mb=2.0, bf16_shadows=True, gather_dtype="bf16", _collectives_at_world1=True, **OPT)
+    x = torch.randint(0, 512, (4, 128), device=DEV, generator=torch.Generator(DEV).manual_seed(1))
+    for model, o, z in ((ref, ref_opt, None), (zero, zero.optimizer, zero)):
+        _step(model, o, z, x)
+    assert zero._masters_stale
+    with torch.no_grad():
+        got = zero(x).float()
+        want = ref(x).float()
+    assert not zero._masters_stale
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
