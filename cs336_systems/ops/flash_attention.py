@@ -148,10 +148,10 @@ def _pad_d(x, Dp):
 
 
 def _padded_d(D, dtype=None):
-    """Head dim the kernels run at: 32/64/128 natively, 80 natively for 16-bit inputs (computed
-    as 96 inside the kernel, no copies); anything else is zero-padded on the host."""
-    if D == 80 and dtype in (torch.bfloat16, torch.float16):
-        return 80
+    """Head dim the kernels run at: 32/64/128 natively, 16 and 80 natively for 16-bit inputs
+    (computed as 32 / 96 inside the kernel, no copies); anything else is zero-padded on the host."""
+    if D in (16, 80) and dtype in (torch.bfloat16, torch.float16):
+        return D
     for s in _SUPPORTED_D:
         if D <= s:
             return s

@@ -44,8 +44,8 @@ void check_bhnd(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.dim() == 4, "cs336: ", name, " must be (B, H, N, D)");
   TORCH_CHECK(t.stride(3) == 1, "cs336: ", name, " must have a contiguous last dim");
   const int D = (int)t.size(3);
-  TORCH_CHECK(D == 32 || D == 64 || D == 128 || (D == 80 && t.element_size() == 2),
-              "cs336: head dim must be 32, 64, 128, or 80 for 16-bit inputs (got ", D, ")");
+  TORCH_CHECK(D == 32 || D == 64 || D == 128 || ((D == 80 || D == 16) && t.element_size() == 2),
+              "cs336: head dim must be 32, 64, 128, or 16 / 80 for 16-bit inputs (got ", D, ")");
   const int64_t es = t.element_size();
   TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) == 0, "cs336: ", name, " must be 16-byte aligned");
   TORCH_CHECK((t.stride(2) * es) % 16 == 0 && (t.stride(1) * es) % 16 == 0 && (t.stride(0) * es) % 16 == 0,

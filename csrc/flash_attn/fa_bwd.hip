@@ -736,6 +736,14 @@ void launch_bwd(const AttnBwdParams& bp, hipStream_t s) {
 template <typename T>
 void launch_bwd_d(const AttnBwdParams& bp, hipStream_t s) {
   switch (bp.f.D) {
+    case 16:  // computed as 32 inside the kernel (d 16..31 zero in LDS, never loaded or stored): no host padding copies
+      if constexpr (std::is_same<T, float>::value) {
+        fprintf(stderr, "fa_bwd: head dim 16 is 16-bit only\n");
+        abort();
+      } else {
+        launch_bwd<T, 16>(bp, s);
+      }
+      break;
     case 32: launch_bwd<T, 32>(bp, s); break;
     case 64: launch_bwd<T, 64>(bp, s); break;
     case 80:

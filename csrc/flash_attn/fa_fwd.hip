@@ -455,6 +455,14 @@ void launch_fwd(const AttnParams& p, hipStream_t s) {
 template <typename T>
 void launch_fwd_d(const AttnParams& p, hipStream_t s) {
   switch (p.D) {
+    case 16:  // computed as 32 inside the kernel (d 16..31 zero in LDS, never loaded or stored): no host padding copies
+      if constexpr (std::is_same<T, float>::value) {
+        fprintf(stderr, "fa_fwd: head dim 16 is 16-bit only\n");
+        abort();
+      } else {
+        launch_fwd<T, 16>(p, s);
+      }
+      break;
     case 32: launch_fwd<T, 32>(p, s); break;
     case 64: launch_fwd<T, 64>(p, s); break;
     case 80:

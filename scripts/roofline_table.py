@@ -90,7 +90,8 @@ def main():
 
 def is_gemm(k: str) -> bool:
     """hipBLASLt/Tensile kernels and the cs336 GEMMs (gemm8 NT with fused epilogues, older gemm)."""
-    return k.startswith("Cijk") or k.startswith("Custom_Cijk") or "gemm8_kernel" in k or "gemm_kernel<" in k
+    return (k.startswith("Cijk") or k.startswith("Custom_Cijk") or "gemm8_kernel" in k or "gemm8w_kernel" in k
+            or "gemm_kernel<" in k)
 
 
 def gemm_roles(step, xf, M, d, f, L, V):
@@ -101,6 +102,7 @@ def gemm_roles(step, xf, M, d, f, L, V):
     fwd = [x for x in g if x[0] < xf]
     bwd = [x for x in g if x[0] >= xf]
     if len(fwd) != 4 * L + 1 or len(bwd) != 8 * L + 2:
+        # (gemm8w runs in the step's own order inside the backward, counted with it here)
         print(f"\n(GEMM order not recognised: {len(fwd)} fwd / {len(bwd)} bwd GEMMs)")
         return
     flops = {"qkv": 2 * M * d * 3 * d, "o": 2 * M * d * d, "w13": 2 * M * d * 2 * f, "w2": 2 * M * f * d, "lm": 2 * M * d * V}
@@ -116,9 +118,13 @@ def gemm_roles(step, xf, M, d, f, L, V):
     fused = any("gemm8_kernel<5, 2>" in k or "gemm8_kernel<4, 2>" in k or "gemm8_kernelILi5ELi2" in k for _, _, k in bwd)
     order = (["w2 dW", "w2 dX", "w13 dX", "w13 dW", "o dX", "o dW", "qkv dX", "qkv dW"] if fused else
              ["w2 dX", "w2 dW", "w13 dX", "w13 dW", "o dX", "o dW", "qkv dX", "qkv dW"])
+    # the lm-head weight gradient may be a gemm8w kernel too: then the first backward GEMM is lm dW
+    lm_order = ("dX", "dW")
+    if bwd and "gemm8w" in bwd[0][2] and len(bwd) > 1 and "gemm8w" not in bwd[1][2]:
+        lm_order = ("dW", "dX")
     for j, (s, e, k) in enumerate(bwd):
         if j < 2:
-            role = "lm " + ("dX", "dW")[j]
+            role = "lm " + lm_order[j]
         else:
             role = order[(j - 2) % 8]
         t[role] += (e - s) / 1e6

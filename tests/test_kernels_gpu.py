@@ -177,6 +177,20 @@ def test_flash_fwd_bwd_d80_native(dt, causal, N):
     _check_flash(dt, 80, causal, N, 2, 3)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("N", [128, 200, 512, 1100])
+def test_flash_fwd_bwd_d16_native(dt, causal, N, monkeypatch):
+    """d_head 16 (the reference's attention sweeps) runs natively (32-wide inside the kernel: no
+    F.pad copies of q/k/v/dO and no slicing of O / the gradients on the host)."""
+    from cs336_systems.ops.flash_attention import _padded_d
+
+    assert _padded_d(16, dt) == 16
+    _check_flash(dt, 16, causal, N, 2, 3)
+    monkeypatch.setenv("CS336_FA_DMA", "2")  # the LDS-DMA staging with the 2 real chunks of 4
+    _check_flash(dt, 16, causal, N, 1, 2)
+
+
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("N", [200, 512])
