@@ -217,7 +217,6 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
                 const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
                 const at::Tensor& dk, const at::Tensor& dv, const OptT& rope_cos, const OptT& rope_sin,
                 const OptT& rope_pos, bool rope_out_only) {
-  at::Tensor delta = at::empty({2, q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
   cs336::AttnBwdParams bp;
   fill_attn(bp.f, q, k, v, out, lse, causal, scale);
   set_rope(bp.f, q, k, rope_cos, rope_sin, rope_pos);
@@ -230,6 +229,26 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
   bp.dq_sb = dq.stride(0); bp.dq_sh = dq.stride(1); bp.dq_sn = dq.stride(2);
   bp.dk_sb = dk.stride(0); bp.dk_sh = dk.stride(1); bp.dk_sn = dk.stride(2);
   bp.dv_sb = dv.stride(0); bp.dv_sh = dv.stride(1); bp.dv_sn = dv.stride(2);
+  // CS336_FA_BWD: unset = the fused one-kernel backward (fa_bwd_fused.hip) where it applies and the
+  // (batch, head) workgroups fill the chip (B·H >= 512); 1 = fused wherever it applies; 0 = the
+  // two-kernel form (dQ kernel + dK/dV kernel)
+  const int mode = [] {
+    const char* e = std::getenv("CS336_FA_BWD");
+    return e && *e ? std::atoi(e) : -1;
+  }();
+  const int64_t nbh = q.size(0) * q.size(1);
+  at::Tensor dq_acc;
+  if (mode != 0 && (mode == 1 || nbh >= 512)) {
+    // partial sums exist only for rows with more than one 256-key block
+    dq_acc = at::empty({q.size(2) > 256 ? nbh * q.size(2) * 64 : 4}, q.options().dtype(at::kFloat));
+    bp.dq_acc = dq_acc.data_ptr<float>();
+    if (cs336::flash_attn_bwd_fused_ok(bp, to_dtype(q))) {
+      cs336::flash_attn_bwd_fused(bp, to_dtype(q), stream());
+      return;
+    }
+    bp.dq_acc = nullptr;
+  }
+  at::Tensor delta = at::empty({2, q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
   bp.delta = delta.data_ptr<float>();
   bp.lrow = bp.delta + q.size(0) * q.size(1) * q.size(2);
   cs336::flash_attn_bwd(bp, to_dtype(q), stream());

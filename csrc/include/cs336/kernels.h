@@ -162,9 +162,14 @@ struct AttnBwdParams {
   // -delta (delta = rowsum(dO * O)) and -lse / scale, loaded as the initial dP and S accumulators
   float* delta;
   float* lrow;
+  // fp32 (B, H, Nq, 64) dQ partial sums of the fused head-sequential backward (fa_bwd_fused.hip)
+  float* dq_acc = nullptr;
 };
 
 void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s);
 void flash_attn_bwd(const AttnBwdParams& p, DType t, hipStream_t s);
+// one-kernel backward, one workgroup per (batch, head): 16-bit, d 64, Nq == Nk, N % 64 == 0, N <= 1024
+bool flash_attn_bwd_fused_ok(const AttnBwdParams& p, DType t);
+void flash_attn_bwd_fused(const AttnBwdParams& p, DType t, hipStream_t s);
 
 }  // namespace cs336

@@ -1,0 +1,95 @@
+"""The fused one-kernel FlashAttention-2 backward (csrc/flash_attn/fa_bwd_fused.hip: one workgroup
+per (batch, head), five MFMA products per tile, dQ summed across key blocks through fp32 partials)
+against an fp64 reference, the two-kernel backward, and the default selection (fused at B·H >= 512)."""
+
+import math
+
+import pytest
+import torch
+
+from cs336_systems.models import RotaryEmbedding
+from cs336_systems.ops._ext import ops as _hip
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ref(q, k, v, do, causal):
+    qr, kr, vr = (t.detach().double().requires_grad_(True) for t in (q, k, v))
+    s = qr @ kr.transpose(-1, -2) / math.sqrt(q.shape[-1])
+    if causal:
+        n = q.shape[-2]
+        s = s.masked_fill(~torch.ones(n, n, dtype=torch.bool, device=q.device).tril(), float("-inf"))
+    o = torch.softmax(s, -1) @ vr
+    o.backward(do.double())
+    return qr.grad, kr.grad, vr.grad
+
+
+def _inputs(B, H, N, dt, seed=0):
+    torch.manual_seed(seed)
+    mk = lambda: torch.randn(B, N, H, 64, device=DEV, dtype=dt).transpose(1, 2)  # noqa: E731
+    return mk(), mk(), mk(), mk()
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("N", [64, 128, 256, 320, 512, 768, 1024])
+def test_fused_bwd_vs_fp64(dt, causal, N, monkeypatch):
+    monkeypatch.setenv("CS336_FA_BWD", "1")
+    B, H = 2, 3
+    q, k, v, do = _inputs(B, H, N, dt)
+    hip = _hip()
+    o, lse = hip.fa_fwd(q, k, v, causal, 0.125)
+    dq, dk, dv = hip.fa_bwd(do, q, k, v, o, lse, causal, 0.125)
+    rq, rk, rv = _ref(q, k, v, do, causal)
+    for a, b, name in ((dq, rq, "dq"), (dk, rk, "dk"), (dv, rv, "dv")):
+        err = (a.double() - b).abs().max().item()
+        scale = b.abs().max().item()
+        assert err <= 2e-2 * max(1.0, scale), f"{name}: max err {err} (ref max {scale})"
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("N", [256, 512, 1024])
+def test_fused_matches_two_kernel(causal, N, monkeypatch):
+    B, H = 3, 5
+    q, k, v, do = _inputs(B, H, N, torch.bfloat16, seed=1)
+    hip = _hip()
+    o, lse = hip.fa_fwd(q, k, v, causal, 0.125)
+    monkeypatch.setenv("CS336_FA_BWD", "0")
+    two = hip.fa_bwd(do, q, k, v, o, lse, causal, 0.125)
+    monkeypatch.setenv("CS336_FA_BWD", "1")
+    fused = hip.fa_bwd(do, q, k, v, o, lse, causal, 0.125)
+    again = hip.fa_bwd(do, q, k, v, o, lse, causal, 0.125)
+    for a, b, c in zip(fused, two, again):
+        assert torch.equal(a, c)  # deterministic: no atomics
+        torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=2e-2)
+
+
+def test_fused_rope_out_only_in_step_layout(monkeypatch):
+    """The XL step's call: dq/dk/dv written into the three slices of one fused d(qkv) buffer, q/k
+    already rotated, inverse RoPE fused into the dQ/dK store; B·H = 600 >= 512 takes the fused
+    kernel by default (bitwise equal to forcing it)."""
+    B, H, N, D = 24, 25, 512, 64
+    torch.manual_seed(2)
+    qkv = torch.randn(B, N, 3, H, D, device=DEV, dtype=torch.bfloat16)
+    q, k, v = qkv[:, :, 0].transpose(1, 2), qkv[:, :, 1].transpose(1, 2), qkv[:, :, 2].transpose(1, 2)
+    do = torch.randn(B, N, H, D, device=DEV, dtype=torch.bfloat16).transpose(1, 2)
+    re = RotaryEmbedding(1024, D, 10000.0).to(DEV)
+    cos, sin = re.cos.contiguous(), re.sin.contiguous()
+    hip = _hip()
+    o, lse = hip.fa_fwd(q, k, v, True, D**-0.5)
+
+    def run():
+        d = torch.empty(B, N, 3, H, D, device=DEV, dtype=torch.bfloat16)
+        dq, dk, dv = d[:, :, 0].transpose(1, 2), d[:, :, 1].transpose(1, 2), d[:, :, 2].transpose(1, 2)
+        hip.fa_bwd_into(do, q, k, v, o, lse, True, D**-0.5, dq, dk, dv, cos, sin, None, True)
+        return d
+
+    monkeypatch.delenv("CS336_FA_BWD", raising=False)
+    default = run()
+    monkeypatch.setenv("CS336_FA_BWD", "1")
+    fused = run()
+    monkeypatch.setenv("CS336_FA_BWD", "0")
+    two = run()
+    assert torch.equal(default, fused)
+    torch.testing.assert_close(fused.float(), two.float(), rtol=2e-2, atol=2e-2)
