@@ -27,10 +27,14 @@ MI355X/RCCL design notes:
   all-reduce of the last bucket at algorithm bandwidth ``w``. It is minimal at
   ``bucket* = sqrt(s·w·o)``. For GPT-2 XL (s = 8.0 GB of fp32 gradients), an 8-rank RCCL ring over
   xGMI (bus bandwidth ≈ 300 GB/s of the 7 × 153 GB/s links ⇒ w = busbw / (2·7/8) ≈ 170 GB/s) and
-  o ≈ 15-30 µs: bucket* ≈ 140-200 MB. 128 MB (64 buckets for XL) sits at the low edge, which keeps
-  the exposed tail of the last bucket (≈ 0.8 ms) small and costs ≈ 1-2 ms of per-collective
-  overhead spread over the backward. ``cs336_systems/bench/collectives.py`` measures ``w`` and
-  ``o`` on the node; only gloo/CPU numbers exist so far (``profiles/r1_allreduce_gloo_cpu.json``).
+  o ≈ 15-30 µs: bucket* ≈ 140-200 MB. Why 128 MB anyway: (1) the model is flat near its optimum —
+  at o = 20 µs the model prices 128 MB at 2.00 ms and the optimum (165 MB) at 1.94 ms, a 0.06 ms
+  difference; (2) the indivisible fused units of one XL layer (W1|W3 82 MB, W2 41 MB, QKV 31 MB, O
+  10 MB, fp32) total ≈ 123 MB, so a 128 MB cap cuts the buckets at layer boundaries (74 buckets of
+  61-127 MB, ``profiles/r3_multirank_rehearsal.jsonl``) and the first all-reduce starts after the
+  last layer's backward instead of one and a half layers in; (3) the exposed tail of the last bucket
+  stays ≈ 0.75 ms. ``bench.py`` at N > 1 appends an fp32 all-reduce sweep (1/10/100/1024 MB: algbw,
+  busbw) to its JSON, from which ``w`` and ``o`` of the real node refit ``bucket*``.
 * Unlike the reference, buckets hold only ``requires_grad`` parameters (no empty bucket 0, frozen
   params never block a flush).
 * Collective order is identical on every rank: buckets are issued strictly in index order (a

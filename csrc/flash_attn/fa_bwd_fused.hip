@@ -28,6 +28,8 @@
 // ahead) and kept with -lse·log2(e) for the whole head in LDS (N ≤ 1024).
 #include "fa_common.h"
 
+#include <cstdlib>
+
 namespace cs336 {
 namespace fa {
 
@@ -50,8 +52,11 @@ constexpr int FLDS = OFF_D + FMAXN * 4;
 static_assert(FLDS <= 160 * 1024, "LDS budget");
 }  // namespace
 
-template <typename T, bool CAUSAL, int ROPE>
+// VAR (A/B switches, CS336_FA_FUSED_VAR): bit 0 = fragment reads batched ahead of their MFMAs
+// (sched_barrier), bit 1 = the dQ product split over all eight waves
+template <typename T, bool CAUSAL, int ROPE, int VAR>
 __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParams bp) {
+  constexpr bool BATCH = VAR & 1, SPLITDQ = VAR & 2;
   typedef typename Elem<T>::storage S;
   typedef typename Mma16<T>::frag F;
   __shared__ __attribute__((aligned(1024))) char smem[FLDS];
@@ -283,7 +288,7 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
             oa[ks] = rowf(dOt, ks);
           }
           f32x16 dp = *reinterpret_cast<const f32x16*>(Ds + 32 * t + 16 * hh);
-          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (BATCH) __builtin_amdgcn_sched_barrier(0);
           f32x16 sa = zero16();
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks) {
@@ -317,7 +322,7 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
           for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt) qt[s2][dt] = trf(Qt + 16 * s2 * FRB, dt);
-          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (BATCH) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -344,10 +349,10 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
       // tile to waves 0-3 through this item's (dead) Q/dO slot
       const int ng = CAUSAL ? min(8, (q0 + FBQ - kbase) / 32) : 8;  // active groups: 0 .. ng-1
       const int nv = min(ng, (N - kbase) / 32);
-      const int g0 = 4 * (wave >> 2), gn = min(nv, g0 + 4);
+      const int g0 = SPLITDQ ? 4 * (wave >> 2) : 0, gn = SPLITDQ ? min(nv, g0 + 4) : (dqw ? nv : 0);
       f32x16 dq = zero16();
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < (SPLITDQ ? 4 : 8); ++u) {
         if (g0 + u >= gn) break;
         const int ro = 32 * (g0 + u) * FRB;
         F ka[2], db[2];
@@ -356,16 +361,17 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
           ka[s2] = trf2(Kimg + ro + 16 * s2 * FRB, kqa, kqb);
           db[s2] = trf2(dsimg + ro + 16 * s2 * FRB, dsa, dsb);
         }
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (BATCH) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) dq = Mma16<T>::mma(ka[s2], db[s2], dq);
       }
-      float* xch = reinterpret_cast<float*>(smem + slot * FSLOT) + (wave & 3) * 1024 + lane * 16;
-      if (nv > 4) {  // workgroup-uniform
+      // [wave & 3][i][lane] float4s: conflict-free 16-B writes and reads
+      float* xch = reinterpret_cast<float*>(smem + slot * FSLOT) + (wave & 3) * 1024 + lane * 4;
+      if (SPLITDQ && nv > 4) {  // workgroup-uniform
         if (!dqw) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<float4*>(xch + 4 * i) = make_float4(dq[4 * i], dq[4 * i + 1], dq[4 * i + 2], dq[4 * i + 3]);
+            *reinterpret_cast<float4*>(xch + 256 * i) = make_float4(dq[4 * i], dq[4 * i + 1], dq[4 * i + 2], dq[4 * i + 3]);
         }
         dma_barrier();
       }
@@ -375,10 +381,10 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
 #pragma unroll
           for (int g4 = 0; g4 < 4; ++g4) pp[g4] = *reinterpret_cast<const float4*>(part + qrow * FD + 8 * g4);
         }
-        if (nv > 4) {
+        if (SPLITDQ && nv > 4) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float4 x = *reinterpret_cast<const float4*>(xch + 4 * i);
+            const float4 x = *reinterpret_cast<const float4*>(xch + 256 * i);
             dq[4 * i] += x.x;
             dq[4 * i + 1] += x.y;
             dq[4 * i + 2] += x.z;
@@ -426,11 +432,28 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
   }
 }
 
+template <typename T, bool C, int V>
+void launch_fused_v(const AttnBwdParams& bp, hipStream_t s) {
+  const dim3 grid((unsigned)(bp.f.B * bp.f.H)), block(512);
+  if (bp.f.rope_cos != nullptr) hipLaunchKernelGGL((fa_bwd_fused_kernel<T, C, 2, V>), grid, block, 0, s, bp);
+  else hipLaunchKernelGGL((fa_bwd_fused_kernel<T, C, 0, V>), grid, block, 0, s, bp);
+}
+
 template <typename T, bool C>
 void launch_fused_c(const AttnBwdParams& bp, hipStream_t s) {
-  const dim3 grid((unsigned)(bp.f.B * bp.f.H)), block(512);
-  if (bp.f.rope_cos != nullptr) hipLaunchKernelGGL((fa_bwd_fused_kernel<T, C, 2>), grid, block, 0, s, bp);
-  else hipLaunchKernelGGL((fa_bwd_fused_kernel<T, C, 0>), grid, block, 0, s, bp);
+  static const int var = [] {
+    const char* e = std::getenv("CS336_FA_FUSED_VAR");
+    return e && *e ? std::atoi(e) : 3;
+  }();
+  if constexpr (std::is_same<T, BF16>::value) {
+    switch (var) {
+      case 0: launch_fused_v<T, C, 0>(bp, s); return;
+      case 1: launch_fused_v<T, C, 1>(bp, s); return;
+      case 2: launch_fused_v<T, C, 2>(bp, s); return;
+      default: break;
+    }
+  }
+  launch_fused_v<T, C, 3>(bp, s);
 }
 
 }  // namespace fa
