@@ -225,7 +225,14 @@ def refresh_transposed(params) -> int:
             n += 1
         else:
             for p in ps:
-                get_shadow_t(p).copy_(get_shadow(p).t())
+                s, st = get_shadow(p), get_shadow_t(p)
+                ok = (s.is_cuda and s.dim() == 2 and st.dim() == 2 and s.stride(1) == 1 and st.stride(1) == 1
+                      and s.shape[0] % 8 == 0 and s.shape[1] % 8 == 0 and s.stride(0) % 8 == 0 and st.stride(0) % 8 == 0
+                      and s.data_ptr() % 16 == 0 and st.data_ptr() % 16 == 0 and ops.ext_available())
+                if ok:
+                    _hip().transpose2d_into(s, st)  # the HIP transpose, not a strided copy
+                else:
+                    st.copy_(s.t())
                 n += 1
         for p in ps:
             mark_shadow_t_synced(p)

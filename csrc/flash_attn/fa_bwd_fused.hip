@@ -15,20 +15,20 @@
 // resident, no atomics, deterministic); the last contributing key block writes dQ (bf16, RoPE-inverse
 // fused). With B·H >> 256 CUs the grid still fills the chip (XL: 1200 workgroups, ~4.7 per CU).
 //
-// Structure (cdna_hip_programming.md "Attention backward"): 4 waves, one per SIMD (≤ 512 registers
-// each); key block = 256 keys; wave w owns the two 32-key groups w and 7 - w of the block (balanced
-// work under the causal mask), keeping dKᵀ/dVᵀ (4 x 32x32 fp32 tiles) in registers and K, V as
-// MFMA B fragments (key on the lane). The workgroup sweeps 64-row query slices staged by LDS-DMA
-// (3-slot ring, prefetched across key-block boundaries):
+// Structure (cdna_hip_programming.md "Attention backward"): 8 waves, two per SIMD (≤ 256 registers
+// each); key block = 256 keys; wave w owns the 32-key group g = w (w < 4) or 11 - w, so the two
+// waves of a SIMD hold groups g and 7 - g (balanced work under the causal mask); each keeps dKᵀ/dVᵀ
+// (2 x 32x32 fp32 tiles) and V (MFMA B fragments, key on the lane) in registers and reads K from the
+// block's LDS image. The workgroup sweeps 64-row query slices staged by LDS-DMA (3-slot ring,
+// prefetched across key-block boundaries), one 32-query tile at a time per wave:
 //   S = Q Kᵀ, dP = dO Vᵀ - delta (row constant as the accumulator's start), P = exp2(S c - L),
 //   dS = P dP, dVᵀ += dOᵀ P, dKᵀ += Qᵀ dS (accumulators as B operands, Q/dO transposed LDS reads),
-//   dSᵀ -> LDS (8-B writes), barrier, dQᵀ tile (32 d x 32 q per wave) = Kᵀ dSᵀ over the block's
-//   active key groups, both operands transposed reads of the K and dSᵀ images.
+//   dSᵀ -> LDS (8-B writes), barrier, then waves 0-3 each form one 32 d x 32 q tile of dQᵀ = Kᵀ dSᵀ
+//   over the block's active key groups (both operands transposed reads of the K and dSᵀ images),
+//   while waves 4-7 compute the next slice's delta during the first key block.
 // delta = rowsum(dO·O) is computed in the first key block's pass (registers prefetched one slice
 // ahead) and kept with -lse·log2(e) for the whole head in LDS (N ≤ 1024).
 #include "fa_common.h"
-
-#include <cstdlib>
 
 namespace cs336 {
 namespace fa {
@@ -52,11 +52,8 @@ constexpr int FLDS = OFF_D + FMAXN * 4;
 static_assert(FLDS <= 160 * 1024, "LDS budget");
 }  // namespace
 
-// VAR (A/B switches, CS336_FA_FUSED_VAR): bit 0 = fragment reads batched ahead of their MFMAs
-// (sched_barrier), bit 1 = the dQ product split over all eight waves
-template <typename T, bool CAUSAL, int ROPE, int VAR>
+template <typename T, bool CAUSAL, int ROPE>
 __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParams bp) {
-  constexpr bool BATCH = VAR & 1, SPLITDQ = VAR & 2;
   typedef typename Elem<T>::storage S;
   typedef typename Mma16<T>::frag F;
   __shared__ __attribute__((aligned(1024))) char smem[FLDS];
@@ -288,8 +285,7 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
             oa[ks] = rowf(dOt, ks);
           }
           f32x16 dp = *reinterpret_cast<const f32x16*>(Ds + 32 * t + 16 * hh);
-          if constexpr (BATCH) __builtin_amdgcn_sched_barrier(0);
-          f32x16 sa = zero16();
+                    f32x16 sa = zero16();
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks) {
             sa = Mma16<T>::mma(qa[ks], kfr[ks], sa);
@@ -322,8 +318,7 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
           for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt) qt[s2][dt] = trf(Qt + 16 * s2 * FRB, dt);
-          if constexpr (BATCH) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
+          #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt) dv[dt] = Mma16<T>::mma(ot[s2][dt], pf[s2], dv[dt]);
@@ -344,51 +339,25 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
       }
       dma_barrier();  // dSᵀ of every group written
 
-      // G: dQᵀ tile = Kᵀ dSᵀ over the active groups (+ the earlier blocks' partial sum). All eight
-      // waves: wave w takes tile (dqt, qqt) over groups 4(w>>2) .. +3; waves 4-7 hand their partial
-      // tile to waves 0-3 through this item's (dead) Q/dO slot
-      const int ng = CAUSAL ? min(8, (q0 + FBQ - kbase) / 32) : 8;  // active groups: 0 .. ng-1
-      const int nv = min(ng, (N - kbase) / 32);
-      const int g0 = SPLITDQ ? 4 * (wave >> 2) : 0, gn = SPLITDQ ? min(nv, g0 + 4) : (dqw ? nv : 0);
-      f32x16 dq = zero16();
-#pragma unroll
-      for (int u = 0; u < (SPLITDQ ? 4 : 8); ++u) {
-        if (g0 + u >= gn) break;
-        const int ro = 32 * (g0 + u) * FRB;
-        F ka[2], db[2];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          ka[s2] = trf2(Kimg + ro + 16 * s2 * FRB, kqa, kqb);
-          db[s2] = trf2(dsimg + ro + 16 * s2 * FRB, dsa, dsb);
-        }
-        if constexpr (BATCH) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) dq = Mma16<T>::mma(ka[s2], db[s2], dq);
-      }
-      // [wave & 3][i][lane] float4s: conflict-free 16-B writes and reads
-      float* xch = reinterpret_cast<float*>(smem + slot * FSLOT) + (wave & 3) * 1024 + lane * 4;
-      if (SPLITDQ && nv > 4) {  // workgroup-uniform
-        if (!dqw) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<float4*>(xch + 256 * i) = make_float4(dq[4 * i], dq[4 * i + 1], dq[4 * i + 2], dq[4 * i + 3]);
-        }
-        dma_barrier();
-      }
+      // G: dQᵀ tile = Kᵀ dSᵀ over the active groups (+ the earlier blocks' partial sum), waves 0-3
+      // (splitting it over all eight waves with a partial-tile hand-off through LDS, or reading all
+      // fragments ahead of the MFMAs, measured slower: profiles/r3_fa_bwd_fused_ab.md)
       if (dqw) {
         float4 pp[4];  // this wave's dQ partial sums from the earlier key blocks (L2)
         if (!first) {
 #pragma unroll
           for (int g4 = 0; g4 < 4; ++g4) pp[g4] = *reinterpret_cast<const float4*>(part + qrow * FD + 8 * g4);
         }
-        if (SPLITDQ && nv > 4) {
+        const int ng = CAUSAL ? min(8, (q0 + FBQ - kbase) / 32) : 8;  // active groups: 0 .. ng-1
+        const int nv = min(ng, (N - kbase) / 32);
+        f32x16 dq = zero16();
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float4 x = *reinterpret_cast<const float4*>(xch + 256 * i);
-            dq[4 * i] += x.x;
-            dq[4 * i + 1] += x.y;
-            dq[4 * i + 2] += x.z;
-            dq[4 * i + 3] += x.w;
+        for (int gg = 0; gg < 8; ++gg) {
+          if (gg >= nv) break;
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int ro = (32 * gg + 16 * s2) * FRB;
+            dq = Mma16<T>::mma(trf2(Kimg + ro, kqa, kqb), trf2(dsimg + ro, dsa, dsb), dq);
           }
         }
         // H: store (lane = query row qrow, registers 4g4..4g4+3 = d 32dqt + 8g4 + 4hh + 0..3)
@@ -432,28 +401,11 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
   }
 }
 
-template <typename T, bool C, int V>
-void launch_fused_v(const AttnBwdParams& bp, hipStream_t s) {
-  const dim3 grid((unsigned)(bp.f.B * bp.f.H)), block(512);
-  if (bp.f.rope_cos != nullptr) hipLaunchKernelGGL((fa_bwd_fused_kernel<T, C, 2, V>), grid, block, 0, s, bp);
-  else hipLaunchKernelGGL((fa_bwd_fused_kernel<T, C, 0, V>), grid, block, 0, s, bp);
-}
-
 template <typename T, bool C>
 void launch_fused_c(const AttnBwdParams& bp, hipStream_t s) {
-  static const int var = [] {
-    const char* e = std::getenv("CS336_FA_FUSED_VAR");
-    return e && *e ? std::atoi(e) : 3;
-  }();
-  if constexpr (std::is_same<T, BF16>::value) {
-    switch (var) {
-      case 0: launch_fused_v<T, C, 0>(bp, s); return;
-      case 1: launch_fused_v<T, C, 1>(bp, s); return;
-      case 2: launch_fused_v<T, C, 2>(bp, s); return;
-      default: break;
-    }
-  }
-  launch_fused_v<T, C, 3>(bp, s);
+  const dim3 grid((unsigned)(bp.f.B * bp.f.H)), block(512);
+  if (bp.f.rope_cos != nullptr) hipLaunchKernelGGL((fa_bwd_fused_kernel<T, C, 2>), grid, block, 0, s, bp);
+  else hipLaunchKernelGGL((fa_bwd_fused_kernel<T, C, 0>), grid, block, 0, s, bp);
 }
 
 }  // namespace fa
