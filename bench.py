@@ -58,7 +58,7 @@ def parse(argv=None):
     ap.add_argument("--model", default="xl")
     ap.add_argument("--ctx", type=int, default=512)
     # 48 x 512 = 24576 tokens per GPU. Per-GPU batch sweep of the XL step on 1x MI355X
-    # (scripts/batch_sweep.sh, profiles/r2_batch_sweep.md): multiples of 24 run the best hipBLASLt
+    # (profiles/r2_batch_sweep.md; scripts/ab.py bench "b24::--batch 24" ...): multiples of 24 run the best hipBLASLt
     # shapes (24 -> 68.5k, 48 -> 69.4-69.7k, 72 -> 68.9k tok/s; 32/40/64/96 -> 65.2-65.8k); 48 also
     # doubles the backward that hides each step's 8 GB of gradient all-reduce under DDP, at 116 GiB.
     ap.add_argument("--batch", type=int, default=int(os.environ.get("CS336_BENCH_BATCH", 48)), help="per-GPU batch")

@@ -610,10 +610,12 @@ class AttentionCore(torch.autograd.Function):
         return qk, t5[:, :, 2].transpose(1, 2)
 
     @staticmethod
-    def forward(ctx, qkv, cos, sin, pos, H, want_ot=False):
+    def forward(ctx, qkv, cos, sin, pos, H, want_ot=False, prerotated=False):
+        # prerotated: the QKV GEMM applied RoPE to q|k in its store (QKVRopeLinearFn); the gradient
+        # this backward returns is still w.r.t. the un-rotated projection output
         qk_in, v = AttentionCore._split(qkv, H)
         hip = _hip()
-        qk = hip.rope(qk_in, cos, sin, pos, False)
+        qk = qk_in if prerotated else hip.rope(qk_in, cos, sin, pos, False)
         q, k = qk[:, :H], qk[:, H:]
         scale = q.shape[-1] ** -0.5
         if want_ot:  # also Oᵀ (H*dk, B*N), the output projection's token-contiguous dW operand
@@ -649,7 +651,43 @@ class AttentionCore(torch.autograd.Function):
         else:
             hip.fa_bwd_into(do, qk[:, :H], qk[:, H:], v, o, lse, True, ctx.scale, dqk[:, :H], dqk[:, H:], dv)
             hip.rope_into(dqk, cos, sin, pos, True, dqk)
-        return dqkv, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None
+
+
+class QKVRopeLinearFn(torch.autograd.Function):
+    """The fused QKV projection with RoPE applied to its q|k columns inside the GEMM's store
+    (``gemm8`` epi 3): removes the separate forward RoPE pass (read + write of q|k per layer).
+
+    The output holds ROTATED q|k, but autograd treats it as the plain projection output: its only
+    consumer is :class:`AttentionCore` with ``prerotated=True``, whose backward returns the gradient
+    w.r.t. the un-rotated q|k (the FA2 backward rotates dQ/dK back in its store), which is what this
+    backward (the plain linear backward of :class:`FusedLinearFn`) needs."""
+
+    @staticmethod
+    def forward(ctx, x, cos, sin, pos, n_heads, *weights):
+        sub = _SubCtx((True, False, *[w.requires_grad for w in weights]))
+        B, N, _ = x.shape
+        dk = weights[0].shape[0] // n_heads
+
+        def mm(x2, w):
+            if gemm.gemm8_ok(x2, w):
+                return gemm.gemm8_rope(x2, w, cos, sin, pos, N, 2 * n_heads * dk, dk)
+            y2 = gemm.mm_nt(x2, w)
+            qk, _ = AttentionCore._split(y2.view(B, N, -1), n_heads)
+            _hip().rope_into(qk, cos, sin, pos, False, qk)
+            return y2
+
+        sub.mm_override = mm
+        y = FusedLinearFn.forward(sub, x, None, *weights)
+        ctx.sub = sub
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx, _, *dws = FusedLinearFn.backward(ctx.sub, dy)
+        ctx.sub._saved = ()
+        ctx.sub = None
+        return (dx, None, None, None, None, *dws)
 
 
 class _SubCtx:

@@ -29,6 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops import gemm as _gemm
 from ..ops.rope import _normalize_pos
 from ..utils.profiling import annotate
 from . import fused
@@ -245,7 +246,12 @@ class CausalMultiHeadSelfAttention(nn.Module):
         if p is None and N > cos.shape[0]:
             return None
         with annotate("qkv_proj"):
-            qkv = fused.fused_linear(x3, *w)  # (B, N, 3*H*dk)
+            # (the Function falls back to GEMM + in-place RoPE where gemm8 does not take the shape)
+            prerot = cdt == torch.bfloat16 and self.d_k % 8 == 0 and _gemm.qkv_rope_enabled()
+            if prerot:  # RoPE on q|k inside the QKV GEMM's store
+                qkv = fused.QKVRopeLinearFn.apply(x3, cos, sin, p, self.num_heads, *w)
+            else:
+                qkv = fused.fused_linear(x3, *w)  # (B, N, 3*H*dk)
         with annotate("attention"):
             want_ot = (
                 fused.attn_out_transposed()
@@ -253,7 +259,7 @@ class CausalMultiHeadSelfAttention(nn.Module):
                 and self.output_proj.weight.requires_grad
                 and torch.is_grad_enabled()
             )
-            return fused.AttentionCore.apply(qkv, cos, sin, p, self.num_heads, want_ot)
+            return fused.AttentionCore.apply(qkv, cos, sin, p, self.num_heads, want_ot, prerot)
 
     def _context_parallel_forward(self, x3, token_positions, B, N):
         """Ring attention over the context-parallel group (``parallel/context_parallel.py``): x3 is

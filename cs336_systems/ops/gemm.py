@@ -224,6 +224,21 @@ def gemm8_swiglu_bwd(dy: torch.Tensor, w2t: torch.Tensor, y: torch.Tensor) -> to
     return out
 
 
+def qkv_rope_enabled() -> bool:
+    """Whether the fused QKV forward applies RoPE in the GEMM's store (gemm8 epi 3): the cs336 GEMMs
+    are in use (``best`` / ``hip`` modes) and ``CS336_QKV_ROPE`` is not ``0``."""
+    return os.environ.get("CS336_QKV_ROPE", "1") != "0" and _mode() in ("best", "hip")
+
+
+def gemm8_rope(x: torch.Tensor, w: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor | None,
+               seq: int, rope_cols: int, dhead: int) -> torch.Tensor:
+    """``x @ w.T`` with the columns below ``rope_cols`` (the q|k heads of a fused QKV projection)
+    rotated by RoPE in the GEMM's store; ``pos``: int64 position per row, or None (row % seq)."""
+    out = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=torch.bfloat16)
+    ops().gemm8_rope(x, w, out, cos, sin, pos, seq, rope_cols, dhead)
+    return out
+
+
 def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``x @ w.T`` (forward of a linear layer; the input gradient through a Wᵀ shadow)."""
     mode = _mode()

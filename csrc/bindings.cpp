@@ -165,6 +165,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_fwd_ot(const at::Tensor& q, co
   return {o, lse, ot};
 }
 
+void rope_into(const at::Tensor& x, const at::Tensor& cos, const at::Tensor& sin, const std::optional<at::Tensor>& pos,
+               bool inverse, const at::Tensor& out);
 void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                 const at::Tensor& out, const at::Tensor& lse, bool causal, double scale, const at::Tensor& dq,
                 const at::Tensor& dk, const at::Tensor& dv, const OptT& rope_cos, const OptT& rope_sin,
@@ -242,8 +244,34 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
     // partial sums exist only for rows with more than one 256-key block
     dq_acc = at::empty({q.size(2) > 256 ? nbh * q.size(2) * 64 : 4}, q.options().dtype(at::kFloat));
     bp.dq_acc = dq_acc.data_ptr<float>();
-    if (cs336::flash_attn_bwd_fused_ok(bp, to_dtype(q))) {
-      cs336::flash_attn_bwd_fused(bp, to_dtype(q), stream());
+    // The fused kernel's own RoPE-inverse store (CS336_FA_FUSED_ROPE=1) measured slower than the
+    // kernel without it plus one in-place inverse-RoPE pass over d(q|k): 0.430 vs 0.373 ms at the XL
+    // shape in the step's fused-QKV layout (scripts/fa_step_layout.py), so the pass is the default.
+    const bool rope_after = bp.f.rope_out_only && [] {
+      const char* e = std::getenv("CS336_FA_FUSED_ROPE");
+      return !(e && e[0] == '1');
+    }();
+    cs336::AttnBwdParams fb = bp;
+    if (rope_after) {
+      fb.f.rope_cos = fb.f.rope_sin = nullptr;
+      fb.f.rope_pos = nullptr;
+      fb.f.rope_out_only = false;
+    }
+    if (cs336::flash_attn_bwd_fused_ok(fb, to_dtype(q))) {
+      cs336::flash_attn_bwd_fused(fb, to_dtype(q), stream());
+      if (rope_after) {
+        // dq and dk adjacent head blocks of one buffer (the fused dQKV layout): one launch over both
+        const int64_t es = dq.element_size();
+        if (dk.strides() == dq.strides() &&
+            static_cast<const char*>(dk.data_ptr()) ==
+                static_cast<const char*>(dq.data_ptr()) + dq.size(1) * dq.stride(1) * es) {
+          const at::Tensor dqk = dq.as_strided({dq.size(0), 2 * dq.size(1), dq.size(2), dq.size(3)}, dq.strides());
+          rope_into(dqk, *rope_cos, *rope_sin, rope_pos, true, dqk);
+        } else {
+          rope_into(dq, *rope_cos, *rope_sin, rope_pos, true, dq);
+          rope_into(dk, *rope_cos, *rope_sin, rope_pos, true, dk);
+        }
+      }
       return;
     }
     bp.dq_acc = nullptr;
@@ -871,6 +899,49 @@ void gemm8(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, int64_t epi,
   TORCH_CHECK(cs336::gemm8::launch(p, (int)epi, (int)fn, stream()), "cs336: gemm8 launch (fn ", fn, ")");
 }
 
+// QKV projection forward with RoPE in the store (gemm8 epi 3): c = a @ b.T with columns < rope_cols
+// rotated (interleaved pairs, d_head dhead) at position pos[row] (pos: int64 per row, or None: row % seq).
+void gemm8_rope(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const at::Tensor& cos, const at::Tensor& sin,
+                const OptT& pos, int64_t seq, int64_t rope_cols, int64_t dhead) {
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  gemm8_check(a, M, K, "a");
+  gemm8_check(b, N, K, "b");
+  gemm8_check(c, M, N, "c");
+  TORCH_CHECK(gemm8_ok(M, N, K, 3, 0), "cs336: gemm8_rope does not take M=", M, " N=", N, " K=", K);
+  TORCH_CHECK(dhead % 8 == 0 && dhead > 0 && rope_cols % dhead == 0 && rope_cols <= N && seq > 0,
+              "cs336: gemm8_rope needs d_head % 8 == 0 and whole rotated heads");
+  TORCH_CHECK(cos.is_cuda() && sin.is_cuda() && cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat &&
+                  cos.is_contiguous() && sin.is_contiguous() && cos.dim() == 2 && cos.size(1) == dhead / 2 &&
+                  sin.sizes() == cos.sizes(),
+              "cs336: gemm8_rope cos/sin must be contiguous fp32 (ctx, d_head/2)");
+  const int64_t* pp = nullptr;
+  if (pos.has_value() && pos->defined()) {
+    TORCH_CHECK(pos->is_cuda() && pos->scalar_type() == at::kLong && pos->is_contiguous() && pos->numel() == M,
+                "cs336: gemm8_rope pos must be contiguous int64 with one entry per row");
+    pp = pos->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(seq <= cos.size(0), "cs336: gemm8_rope seq ", seq, " exceeds the RoPE cache ", cos.size(0));
+  }
+  cs336::gemm8::Args p{};
+  p.a = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  p.b = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  p.c = reinterpret_cast<uint16_t*>(c.data_ptr());
+  p.lda = a.stride(0);
+  p.ldb = b.stride(0);
+  p.ldc = c.stride(0);
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.rcos = cos.data_ptr<float>();
+  p.rsin = sin.data_ptr<float>();
+  p.rpos = pp;
+  p.rseq = (int)seq;
+  p.rope_cols = (int)rope_cols;
+  p.rdh = (int)dhead;
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(cs336::gemm8::launch(p, 3, 0, stream()), "cs336: gemm8_rope launch");
+}
+
 // Weight gradient straight from token-major operands (csrc/gemm/gemm8w.hip):
 //   out[m][n] (+)= Σ_t a[t][m]·b[t][n]    (trans_out: out[n][m])
 // a (K, M) and b (K, N) bf16 with unit column stride; out fp32 (M, N) or (N, M) with unit column
@@ -962,6 +1033,7 @@ TORCH_LIBRARY(cs336, m) {
   m.def("cohort(int n_workgroups, int lds_bytes, float deadline_ms, Tensor(a!) state) -> ()");
   m.def("gemm8(Tensor a, Tensor b, Tensor(a!) c, int epi, int fn, Tensor(b!)? h, Tensor? y, int half) -> ()");
   m.def("gemm8_ok(int M, int N, int K, int epi, int half) -> bool", &gemm8_ok);
+  m.def("gemm8_rope(Tensor a, Tensor b, Tensor(a!) c, Tensor cos, Tensor sin, Tensor? pos, int seq, int rope_cols, int dhead) -> ()");
   m.def("gemm8w(Tensor a, Tensor b, Tensor(a!) out, int splits, bool trans_out, bool accumulate, int fn) -> ()");
   m.def("multi_tensor_scale_(Tensor(a!)[] tensors, Tensor scale) -> ()");
 }
@@ -995,6 +1067,7 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("occupy", &occupy);
   m.impl("cohort", &cohort);
   m.impl("gemm8", &gemm8);
+  m.impl("gemm8_rope", &gemm8_rope);
   m.impl("gemm8w", &gemm8w);
   m.impl("multi_tensor_scale_", &multi_tensor_scale_);
 }

@@ -13,6 +13,8 @@ namespace gemm8 {
 //        h = silu(a)·b [M][half] (ldh).
 // epi 2 (W2 input gradient): N = half; dh = A·Bᵀ is not stored; reads y = [a|b] (ldy) and writes
 //        C = [da|db] [M][2·half] (ldc).
+// epi 3 (QKV forward + RoPE): C [M][N] with columns < rope_cols rotated in interleaved pairs by
+//        the fp32 (ctx, rdh/2) cos/sin tables at position rpos[row] (or row % rseq when rpos is null).
 // Requires M % 256 == 0, K % 64 == 0, N % (64·fn) == 0 (epi 1: half % (32·fn) == 0), 16-B aligned
 // rows; fn = 5 (BN 320) or 4 (BN 256), 0 = pick.
 struct Args {
@@ -24,6 +26,11 @@ struct Args {
   int64_t lda, ldb, ldc, ldh, ldy;
   int M, N, K;
   int half;
+  // epi 3
+  const float* rcos;
+  const float* rsin;
+  const int64_t* rpos;
+  int rseq, rope_cols, rdh;
 };
 int pick_fn(int N, int epi, int half);
 bool launch(const Args& p, int epi, int fn, hipStream_t s);

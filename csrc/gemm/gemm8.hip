@@ -10,6 +10,9 @@
 //          h = silu(a)·b (the W2 input) -- no separate SwiGLU pass over the 2·d_ff activation
 //   EPI 2  W2 input gradient: dh = dY·W2 is never stored; the epilogue reads the saved a, b and writes
 //          da = dh·b·silu'(a), db = dh·silu(a) into [da|db] (the W1|W3 output gradient)
+//   EPI 3  QKV forward with RoPE: C = A·Bᵀ (bf16) with the interleaved-pair rotation applied to the
+//          columns below rope_cols (q|k heads) in the store -- no separate RoPE pass over q|k. The
+//          rotation reads the bf16-rounded product, as the separate pass did (same rounding points).
 //
 // Structure (cdna_hip_programming.md §5 "256² 8-phase template", re-derived for these shapes):
 // * tile 256 × BN (BN = 64·FN: 256 or 320 -- every N of the XL/2.7b projections is a multiple of
@@ -280,8 +283,24 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
     constexpr int PR = 32, UNITS = PR * CPR, PER = UNITS / 64;
     static_assert(UNITS % 64 == 0, "epilogue units must fill the wave");
     char* scr = smem + wave * (PR * WTN * 4);
+    constexpr int NP = 8 / (PR / 16);  // pieces
+    // a/b loads software-pipelined one piece ahead (two register buffers): a piece's loads are in
+    // flight while the previous piece is computed and stored, so the tile pays about one load
+    // latency instead of one per piece
+    uint4 av[2][PER], bv[2][PER];
+    auto load_ab = [&](int piece, uint4 (&ab)[PER], uint4 (&bb)[PER]) {
 #pragma unroll
-    for (int piece = 0; piece < 8 / (PR / 16); ++piece) {
+      for (int u = 0; u < PER; ++u) {
+        const int q = lane + 64 * u, rr = q / CPR, cc = q % CPR;
+        const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
+        const int col = n0 + bcol + cc * 8;
+        ab[u] = *reinterpret_cast<const uint4*>(p.y + row * p.ldy + col);
+        bb[u] = *reinterpret_cast<const uint4*>(p.y + row * p.ldy + p.half + col);
+      }
+    };
+    load_ab(0, av[0], bv[0]);
+#pragma unroll
+    for (int piece = 0; piece < NP; ++piece) {
 #pragma unroll
       for (int ib = 0; ib < PR / 16; ++ib)
 #pragma unroll
@@ -290,16 +309,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
           *reinterpret_cast<f32x4*>(scr + ((16 * ib + m_l) * WTN + 16 * j + n_l) * 4) = v;
         }
       __builtin_amdgcn_wave_barrier();
-      // all of this piece's a/b loads first (10 x 16 B per lane in flight), then the math
-      uint4 av[PER], bv[PER];
-#pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int q = lane + 64 * u, rr = q / CPR, cc = q % CPR;
-        const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
-        const int col = n0 + bcol + cc * 8;
-        av[u] = *reinterpret_cast<const uint4*>(p.y + row * p.ldy + col);
-        bv[u] = *reinterpret_cast<const uint4*>(p.y + row * p.ldy + p.half + col);
-      }
+      if (piece + 1 < NP) load_ab(piece + 1, av[(piece + 1) & 1], bv[(piece + 1) & 1]);
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
         const int q = lane + 64 * u, rr = q / CPR, cc = q % CPR;
@@ -308,8 +318,8 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
         const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
         const int col = n0 + bcol + cc * 8;
         const float dh[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-        const bf16_t* ae = reinterpret_cast<const bf16_t*>(&av[u]);
-        const bf16_t* be = reinterpret_cast<const bf16_t*>(&bv[u]);
+        const bf16_t* ae = reinterpret_cast<const bf16_t*>(&av[piece & 1][u]);
+        const bf16_t* be = reinterpret_cast<const bf16_t*>(&bv[piece & 1][u]);
         uint4 dav, dbv;
         bf16_t* da = reinterpret_cast<bf16_t*>(&dav);
         bf16_t* db = reinterpret_cast<bf16_t*>(&dbv);
@@ -355,6 +365,26 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
         const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
         if constexpr (EPI == 0) {
           *reinterpret_cast<uint4*>(p.c + row * p.ldc + n0 + bcol + cc * 8) = v;
+        } else if constexpr (EPI == 3) {
+          const int col = n0 + bcol + cc * 8;
+          uint4 o = v;
+          if (col < p.rope_cols) {  // q|k: rotate pairs (2i, 2i+1), i = (col mod d_head) / 2 + 0..3
+            const int64_t pos = p.rpos ? p.rpos[row] : (int64_t)((int)row % p.rseq);
+            const int i0 = (col % p.rdh) >> 1;
+            const float4 c4 = *reinterpret_cast<const float4*>(p.rcos + pos * (p.rdh >> 1) + i0);
+            const float4 s4 = *reinterpret_cast<const float4*>(p.rsin + pos * (p.rdh >> 1) + i0);
+            const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            uint32_t r[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float x0 = bf16_to_f32((bf16_t)(w[e] & 0xffff)), x1 = bf16_to_f32((bf16_t)(w[e] >> 16));
+              r[e] = (uint32_t)f32_to_bf16(cv[e] * x0 - sv[e] * x1) |
+                     ((uint32_t)f32_to_bf16(sv[e] * x0 + cv[e] * x1) << 16);
+            }
+            o = make_uint4(r[0], r[1], r[2], r[3]);
+          }
+          *reinterpret_cast<uint4*>(p.c + row * p.ldc + col) = o;
         } else {
           // tile col tc: a side (wc < 2) -> y[:, n0 + tc], b side -> y[:, half + n0 + tc - BN/2]
           const int tc = bcol + cc * 8;
@@ -432,10 +462,12 @@ bool launch(const Args& p, int epi, int fn, hipStream_t s) {
     if (epi == 0) CS336_G8(5, 0);
     if (epi == 1) CS336_G8(5, 1);
     if (epi == 2) CS336_G8(5, 2);
+    if (epi == 3) CS336_G8(5, 3);
   } else {
     if (epi == 0) CS336_G8(4, 0);
     if (epi == 1) CS336_G8(4, 1);
     if (epi == 2) CS336_G8(4, 2);
+    if (epi == 3) CS336_G8(4, 3);
   }
 #undef CS336_G8
   return false;

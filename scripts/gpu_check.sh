@@ -1,0 +1,41 @@
+#!/bin/bash
+# One gpurun call, staged checks; replaces final_check.sh / session_end_check.sh /
+# gpu_suite_bench_prof.sh / fa_suite_bench.sh. Each GPU step runs under its own time limit and the
+# chain stops at the first failure (nothing else touches a sick GPU).
+#   bash scripts/gpu_check.sh suite bench 2p7b prof flash leaderboard rehearse
+# stages: suite (pytest -m gpu), bench (XL default, 20 steps), 2p7b (2.7b ctx 1024 batch 12),
+#         prof (rocprofv3 kernel trace of the XL step -> roofline + step sequence; PROF_TAG names it),
+#         flash (FA2 at N 4096, d 64/128), leaderboard ((16,16384,64) causal fwd+bwd, cold caches),
+#         rehearse (2 ranks on one GPU over gloo through bench.py)
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+for stage in "$@"; do
+  case $stage in
+    suite)
+      timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_suite.log 2>&1 || { tail -40 gpurun_out/gpu_suite.log; exit 1; }
+      tail -1 gpurun_out/gpu_suite.log ;;
+    bench)
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_xl.json 2> gpurun_out/bench_xl.err || { tail -20 gpurun_out/bench_xl.err; exit 1; }
+      cat gpurun_out/bench_xl.json ;;
+    2p7b)
+      timeout -k 10 300 python bench.py --model 2.7b --ctx 1024 --batch 12 --steps 10 --warmup 3 > gpurun_out/bench_2p7b.json 2> gpurun_out/bench_2p7b.err || { tail -20 gpurun_out/bench_2p7b.err; exit 1; }
+      cut -c1-220 gpurun_out/bench_2p7b.json ;;
+    prof)
+      bash scripts/prof_xl_step.sh || exit 1
+      head -16 gpurun_out/xl_roofline${PROF_TAG:-}.md ;;
+    flash)
+      timeout -k 10 300 python -m cs336_systems.bench.flash --impls hip_fa2 --no-compile --json gpurun_out/flash4096.json > gpurun_out/flash4096.log 2>&1 || { tail gpurun_out/flash4096.log; exit 1; }
+      python -c "
+import json
+for r in json.load(open('gpurun_out/flash4096.json')):
+    print(r['impl'], r['N'], r['d'], r['causal'], 'fwd', round(r['fwd_tflops']), 'bwd', round(r['bwd_tflops']))" ;;
+    leaderboard)
+      timeout -k 10 300 python -m cs336_systems.bench.flash --leaderboard --impls hip_fa2 --json gpurun_out/flash_leaderboard.json > gpurun_out/flash_lb.log 2>&1 || { tail gpurun_out/flash_lb.log; exit 1; }
+      cat gpurun_out/flash_leaderboard.json ;;
+    rehearse)
+      timeout -k 10 300 bash scripts/rehearse_multirank.sh > gpurun_out/rehearse.log 2>&1 || { tail -30 gpurun_out/rehearse.log; exit 1; }
+      grep '"metric"' gpurun_out/rehearse.log | cut -c1-300 ;;
+    *) echo "unknown stage $stage"; exit 2 ;;
+  esac
+done
