@@ -670,7 +670,7 @@ class QKVRopeLinearFn(torch.autograd.Function):
         dk = weights[0].shape[0] // n_heads
 
         def mm(x2, w):
-            if gemm.gemm8_ok(x2, w):
+            if dk <= 96 and gemm.gemm8_ok(x2, w, 3, 2 * n_heads * dk):
                 return gemm.gemm8_rope(x2, w, cos, sin, pos, N, 2 * n_heads * dk, dk)
             y2 = gemm.mm_nt(x2, w)
             qk, _ = AttentionCore._split(y2.view(B, N, -1), n_heads)

@@ -855,9 +855,12 @@ bool gemm8_check(const at::Tensor& t, int64_t rows, int64_t cols, const char* wh
   return true;
 }
 
+// epi 3: `half` carries rope_cols, which must cover whole column tiles (the rotation is decided per
+// tile); the binding also needs d_head <= 96 (the tile rows' cos/sin fit the LDS behind the scratch)
 bool gemm8_ok(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t half) {
   const int fn = cs336::gemm8::pick_fn((int)N, (int)epi, (int)half);
-  return fn != 0 && M % 256 == 0 && K % 64 == 0 && K >= 64 && N % (64 * fn) == 0 && M < (1 << 30);
+  return fn != 0 && M % 256 == 0 && K % 64 == 0 && K >= 64 && N % (64 * fn) == 0 && M < (1 << 30) &&
+         (epi != 3 || half % (64 * fn) == 0);
 }
 
 void gemm8(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, int64_t epi, int64_t fn, const OptT& h,
@@ -907,9 +910,10 @@ void gemm8_rope(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const a
   gemm8_check(a, M, K, "a");
   gemm8_check(b, N, K, "b");
   gemm8_check(c, M, N, "c");
-  TORCH_CHECK(gemm8_ok(M, N, K, 3, 0), "cs336: gemm8_rope does not take M=", M, " N=", N, " K=", K);
-  TORCH_CHECK(dhead % 8 == 0 && dhead > 0 && rope_cols % dhead == 0 && rope_cols <= N && seq > 0,
-              "cs336: gemm8_rope needs d_head % 8 == 0 and whole rotated heads");
+  TORCH_CHECK(gemm8_ok(M, N, K, 3, rope_cols), "cs336: gemm8_rope does not take M=", M, " N=", N, " K=", K,
+              " rope_cols=", rope_cols);
+  TORCH_CHECK(dhead % 8 == 0 && dhead > 0 && dhead <= 96 && rope_cols % dhead == 0 && rope_cols <= N && seq > 0,
+              "cs336: gemm8_rope needs d_head % 8 == 0, d_head <= 96 and whole rotated heads");
   TORCH_CHECK(cos.is_cuda() && sin.is_cuda() && cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat &&
                   cos.is_contiguous() && sin.is_contiguous() && cos.dim() == 2 && cos.size(1) == dhead / 2 &&
                   sin.sizes() == cos.sizes(),

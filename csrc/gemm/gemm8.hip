@@ -337,17 +337,53 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
       lgkm0();  // this piece's scratch reads retired before the next piece's writes
     }
   } else {
-    // bf16 in 64-row pieces: scratch 64 × WTN × 2 B per wave (≤ 80 KiB in all)
-    constexpr int PR = 64, UNITS = PR * CPR, PER = UNITS / 64;
+    // bf16 in 64-row pieces: scratch 64 × WTN × 2 B per wave (≤ 80 KiB in all); EPI 3: 32-row
+    // pieces (40 KiB), and the tile rows' RoPE cos/sin staged in the LDS behind them, so the store
+    // loop reads no global memory (a global load there waits for every earlier store: vmcnt retires
+    // in issue order)
+    constexpr int PR = EPI == 3 ? 32 : 64, UNITS = PR * CPR, PER = UNITS / 64;
     static_assert(UNITS % 64 == 0, "epilogue units must fill the wave");
     char* scr = smem + wave * (PR * WTN * 2);
+    constexpr int TOFF = 8 * PR * WTN * 2;  // EPI 3 table: cos [256][np], then sin [256][np] (fp32)
+    const int np = EPI == 3 ? (p.rdh >> 1) : 0;
+    const bool rot = EPI == 3 && n0 < p.rope_cols;  // tile-uniform (host: rope_cols % BN == 0)
+    if constexpr (EPI == 3) {
+      static_assert(TOFF + 2 * 256 * 48 * 4 <= 2 * STAGE, "cos/sin table of d_head <= 96 behind the scratch");
+      if (rot) {
+        // two threads per tile row, each half of the row's np/4 float4 of cos and of sin: every load
+        // issued before any is waited for (d_head <= 96: at most 6 float4 per thread and table)
+        constexpr int MAXQ = 6;
+        float* tc = reinterpret_cast<float*>(smem + TOFF);
+        float* ts = tc + 256 * np;
+        const int r = tid >> 1, q4n = np >> 2, hq = (q4n + 1) >> 1;
+        const int qb = (tid & 1) * hq;
+        const int row = m0 + r;
+        const int64_t pos = p.rpos ? p.rpos[row] : (int64_t)(row % p.rseq);
+        // indices past this thread's share are clamped to the row's last float4: a duplicate load
+        // and an identical rewrite, never a branch (keeps the arrays in registers)
+        float4 cb[MAXQ], sb[MAXQ];
 #pragma unroll
-    for (int piece = 0; piece < 2; ++piece) {
+        for (int q = 0; q < MAXQ; ++q) {
+          const int i4 = min(qb + q, q4n - 1);
+          cb[q] = *reinterpret_cast<const float4*>(p.rcos + pos * np + 4 * i4);
+          sb[q] = *reinterpret_cast<const float4*>(p.rsin + pos * np + 4 * i4);
+        }
 #pragma unroll
-      for (int ib = 0; ib < 4; ++ib)
+        for (int q = 0; q < MAXQ; ++q) {
+          const int i4 = min(qb + q, q4n - 1);
+          *reinterpret_cast<float4*>(tc + r * np + 4 * i4) = cb[q];
+          *reinterpret_cast<float4*>(ts + r * np + 4 * i4) = sb[q];
+        }
+        __syncthreads();
+      }
+    }
+#pragma unroll
+    for (int piece = 0; piece < 128 / PR; ++piece) {
+#pragma unroll
+      for (int ib = 0; ib < PR / 16; ++ib)
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-          const f32x4 v = acc[piece * 4 + ib][j];
+          const f32x4 v = acc[piece * (PR / 16) + ib][j];
           const uint32_t lo = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
           const uint32_t hi = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
           *reinterpret_cast<uint2*>(scr + ((16 * ib + m_l) * WTN + 16 * j + n_l) * 2) = make_uint2(lo, hi);
@@ -368,11 +404,11 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
         } else if constexpr (EPI == 3) {
           const int col = n0 + bcol + cc * 8;
           uint4 o = v;
-          if (col < p.rope_cols) {  // q|k: rotate pairs (2i, 2i+1), i = (col mod d_head) / 2 + 0..3
-            const int64_t pos = p.rpos ? p.rpos[row] : (int64_t)((int)row % p.rseq);
-            const int i0 = (col % p.rdh) >> 1;
-            const float4 c4 = *reinterpret_cast<const float4*>(p.rcos + pos * (p.rdh >> 1) + i0);
-            const float4 s4 = *reinterpret_cast<const float4*>(p.rsin + pos * (p.rdh >> 1) + i0);
+          if (rot) {  // q|k: rotate pairs (2i, 2i+1), i = (col mod d_head) / 2 + 0..3
+            const int i0 = (col % p.rdh) >> 1, tr = arow + PR * piece + rr;
+            const float* tc = reinterpret_cast<const float*>(smem + TOFF);
+            const float4 c4 = *reinterpret_cast<const float4*>(tc + tr * np + i0);
+            const float4 s4 = *reinterpret_cast<const float4*>(tc + 256 * np + tr * np + i0);
             const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, sv[4] = {s4.x, s4.y, s4.z, s4.w};
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
             uint32_t r[4];

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--gemm8-only", action="store_true", help="time gemm8 alone (variant A/B)")
     args = ap.parse_args()
     from cs336_systems import ops
 
@@ -61,9 +62,11 @@ def main():
             "blas": lambda: torch.mm(a, b.t()),
             "lt": lambda: cs.lt_gemm(a, b, False, True, torch.bfloat16),
         }
-        if epi == 1:  # unfused reference pipeline: GEMM + SwiGLU kernel
+        if args.gemm8_only:
+            cands = {"gemm8": cands["gemm8"]}
+        elif epi == 1:  # unfused reference pipeline: GEMM + SwiGLU kernel
             cands["blas+swiglu"] = lambda: cs.swiglu_fused_fwd(torch.mm(a, b.t()))
-        if epi == 2:
+        if epi == 2 and not args.gemm8_only:
             cands["blas+swiglu_bwd"] = lambda: cs.swiglu_fused_bwd(torch.mm(a, b.t()), y)
         times = {k: [] for k in cands}
         for _ in range(args.rounds):

@@ -46,8 +46,8 @@ def _rope_ref(y, cos, sin, pos, rope_cols, dk):
 def test_gemm8_rope_kernel(B, N, H, dk, K, given_pos):
     cs = _cs()
     M, Nout = B * N, 3 * H * dk
-    if not cs.gemm8_ok(M, Nout, K, 3, 0):
-        pytest.skip("gemm8 does not tile this shape")
+    if not cs.gemm8_ok(M, Nout, K, 3, 2 * H * dk) or dk > 96:
+        pytest.skip("gemm8 epi 3 does not take this shape")
     x, w = _rand(M, K, seed=1), _rand(Nout, K, scale=0.1, seed=2)
     cos, sin = _tables(max(N, 600), dk)
     if given_pos:
