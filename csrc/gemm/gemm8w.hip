@@ -138,11 +138,17 @@ __global__ __launch_bounds__(NT, 2) void gemm8w_kernel(const WArgs p) {
   }
   const int nb_h0 = (G::GB_HI == G::GB_LO || wr == 0) ? G::GB_HI : G::GB_LO;  // B granules in half 0
   const int nb_h1 = (G::GB_HI == G::GB_LO || wr == 1) ? G::GB_HI : G::GB_LO;
-  // (DMA through this by-reference wrapper: with the builtin called on the local descriptor
-  // directly, hipcc (ROCm 7.2) silently dropped this kernel's host stub -- found by bisection)
+  // LDS-DMA in inline asm (M0 = the wave-uniform LDS address; nothing else in this kernel writes
+  // M0): issued through the builtin, the DMA is a pending LDS write the compiler cannot tell from the
+  // transposed fragment reads, so it would need asm reads (below) whose results it must then copy
+  // into the MFMA operand registers -- 4 v_mov per MFMA, measured 1.4x the VALU and 1.37x the wave
+  // cycles of gemm8 on the same FLOPs (profiles/r3_gemm8w_pmc.md)
   const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
   auto glds = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t vo, uint32_t so, uint32_t lds_off) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(smem + lds_off), 16, vo, so, 0, 0);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen lds"
+                 :
+                 : "v"(vo), "s"(lds_base + lds_off), "s"(rs), "s"(so)
+                 : "memory");
   };
 #define CS336_G8W_ISSUE(H, KT, ST)                                                                          \
   do {                                                                                                     \
@@ -159,28 +165,17 @@ __global__ __launch_bounds__(NT, 2) void gemm8w_kernel(const WArgs p) {
 
   // ---- transposed fragment reads ------------------------------------------------------------
   const int g4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-  // Each fragment = two ds_read_b64_tr_b16 issued in inline asm. Through the intrinsic, hipcc puts
-  // s_waitcnt vmcnt(0) in front of every transposed read (it cannot tell them from the pending
-  // LDS-DMA writes), which drains the whole prefetch each phase (measured: waves parked 70 % of
-  // their cycles). In asm the only wait is the phase's explicit lgkmcnt(0), which also takes every
-  // read result as an in/out operand, so no copy of a result can be scheduled before it.
+  // Each fragment = two ds_read_b64_tr_b16 (builtin) joined into one 128-bit MFMA operand; the
+  // phase's explicit lgkmcnt(0) before its barrier retires them (WAR against the DMA restaging)
   auto tr = [&](uint32_t img, int S, int c0, int t) -> s16x4 {
     const int s = c0 >> 4, f = S == SA ? swz<SA>(t) : swz<SB>(t);
-    const uint32_t addr = lds_base + img + (uint32_t)(t * S + ((s ^ f) << 5) + 8 * pp);
-    s16x4 r;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
-    return r;
+    const uint32_t off = img + (uint32_t)(t * S + ((s ^ f) << 5) + 8 * pp);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + off));
   };
-  auto frag2 = [&](uint32_t img, int S, int c0, int ks, s16x4& lo, s16x4& hi) {
+  auto frag = [&](uint32_t img, int S, int c0, int ks) -> bf16x8 {
     const int t0 = 32 * ks + 8 * g4 + q;
-    lo = tr(img, S, c0, t0);
-    hi = tr(img, S, c0, t0 + 4);
-  };
-  auto join = [](const s16x4& lo, const s16x4& hi) -> bf16x8 {
-    s16x8 v;
-    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-    return __builtin_bit_cast(bf16x8, v);
+    const s16x4 lo = tr(img, S, c0, t0), hi = tr(img, S, c0, t0 + 4);
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
 
   f32x4 acc[8][FN];
@@ -189,31 +184,9 @@ __global__ __launch_bounds__(NT, 2) void gemm8w_kernel(const WArgs p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 fa[4], fb[FN];
-  s16x4 al[4], ah[4], bl[FN], bh[FN];
   const int arow = wr * 128, bcol = wc * WTN;
-  // lgkmcnt(0) with the phase's read results as in/out operands (see tr above)
-  auto wait_a = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al[0]), "+v"(ah[0]), "+v"(al[1]), "+v"(ah[1]), "+v"(al[2]), "+v"(ah[2]),
-                 "+v"(al[3]), "+v"(ah[3])::"memory");
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = join(al[i], ah[i]);
-  };
-  auto wait_ab = [&]() {
-    if constexpr (FN == 5)
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(al[0]), "+v"(ah[0]), "+v"(al[1]), "+v"(ah[1]), "+v"(al[2]), "+v"(ah[2]), "+v"(al[3]),
-                     "+v"(ah[3]), "+v"(bl[0]), "+v"(bh[0]), "+v"(bl[1]), "+v"(bh[1]), "+v"(bl[2]), "+v"(bh[2]),
-                     "+v"(bl[3]), "+v"(bh[3]), "+v"(bl[FN - 1]), "+v"(bh[FN - 1])::"memory");
-    else
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(al[0]), "+v"(ah[0]), "+v"(al[1]), "+v"(ah[1]), "+v"(al[2]), "+v"(ah[2]), "+v"(al[3]),
-                     "+v"(ah[3]), "+v"(bl[0]), "+v"(bh[0]), "+v"(bl[1]), "+v"(bh[1]), "+v"(bl[2]), "+v"(bh[2]),
-                     "+v"(bl[FN - 1]), "+v"(bh[FN - 1])::"memory");
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = join(al[i], ah[i]);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) fb[j] = join(bl[j], bh[j]);
-  };
+  auto wait_a = [&]() { lgkm0(); };
+  auto wait_ab = [&]() { lgkm0(); };
 
   auto mma = [&](int i0) {
     __builtin_amdgcn_s_setprio(1);
@@ -249,16 +222,16 @@ __global__ __launch_bounds__(NT, 2) void gemm8w_kernel(const WArgs p) {
     // P0: k 0-31, rows 0-63 (+ all column tiles); restage K-tile t+1's second half
     if (t + 1 < nkt) CS336_G8W_ISSUE(1, t + 1, (t + 1) & 1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) frag2(st, SA, arow + 16 * i, 0, al[i], ah[i]);
+    for (int i = 0; i < 4; ++i) fa[i] = frag(st, SA, arow + 16 * i, 0);
 #pragma unroll
-    for (int j = 0; j < FN; ++j) frag2(st + G::A_BYTES, SB, bcol + 16 * j, 0, bl[j], bh[j]);
+    for (int j = 0; j < FN; ++j) fb[j] = frag(st + G::A_BYTES, SB, bcol + 16 * j, 0);
     wait_ab();
     sbarrier();
     mma(0);
     sbarrier();
     // P1: k 0-31, rows 64-127
 #pragma unroll
-    for (int i = 0; i < 4; ++i) frag2(st, SA, arow + 64 + 16 * i, 0, al[i], ah[i]);
+    for (int i = 0; i < 4; ++i) fa[i] = frag(st, SA, arow + 64 + 16 * i, 0);
     wait_a();
     sbarrier();
     mma(4);
@@ -266,16 +239,16 @@ __global__ __launch_bounds__(NT, 2) void gemm8w_kernel(const WArgs p) {
     // P2: k 32-63, rows 0-63; restage this stage's first half with K-tile t+2
     if (t + 2 < nkt) CS336_G8W_ISSUE(0, t + 2, t & 1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) frag2(st, SA, arow + 16 * i, 1, al[i], ah[i]);
+    for (int i = 0; i < 4; ++i) fa[i] = frag(st, SA, arow + 16 * i, 1);
 #pragma unroll
-    for (int j = 0; j < FN; ++j) frag2(st + G::A_BYTES, SB, bcol + 16 * j, 1, bl[j], bh[j]);
+    for (int j = 0; j < FN; ++j) fb[j] = frag(st + G::A_BYTES, SB, bcol + 16 * j, 1);
     wait_ab();
     sbarrier();
     mma(0);
     sbarrier();
     // P3: k 32-63, rows 64-127; retire K-tile t+1 (only K-tile t+2's first half may stay in flight)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) frag2(st, SA, arow + 64 + 16 * i, 1, al[i], ah[i]);
+    for (int i = 0; i < 4; ++i) fa[i] = frag(st, SA, arow + 64 + 16 * i, 1);
     if (t + 1 < nkt) {
       if (t + 2 < nkt) {
         if (big0) vmcnt<G::GA + G::GB_HI>();
