@@ -244,13 +244,10 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
     // partial sums exist only for rows with more than one 256-key block
     dq_acc = at::empty({q.size(2) > 256 ? nbh * q.size(2) * 64 : 4}, q.options().dtype(at::kFloat));
     bp.dq_acc = dq_acc.data_ptr<float>();
-    // The fused kernel's own RoPE-inverse store (CS336_FA_FUSED_ROPE=1) measured slower than the
-    // kernel without it plus one in-place inverse-RoPE pass over d(q|k): 0.430 vs 0.373 ms at the XL
-    // shape in the step's fused-QKV layout (scripts/fa_step_layout.py), so the pass is the default.
-    const bool rope_after = bp.f.rope_out_only && [] {
-      const char* e = std::getenv("CS336_FA_FUSED_ROPE");
-      return !(e && e[0] == '1');
-    }();
+    // RoPE (dQ/dK w.r.t. the un-rotated q, k) as one in-place inverse pass over d(q|k) after the fused
+    // kernel: a rotating store inside it measured slower (0.430 vs 0.373 ms at the XL shape in the
+    // step's fused-QKV layout, scripts/fa_step_layout.py; profiles/r3_qkv_rope_ab.md)
+    const bool rope_after = bp.f.rope_out_only;
     cs336::AttnBwdParams fb = bp;
     if (rope_after) {
       fb.f.rope_cos = fb.f.rope_sin = nullptr;

@@ -12,8 +12,9 @@
 // floor alone (1.5 x the fp32 dQ bytes) is ~180 us per XL layer. Here ONE workgroup owns a whole
 // (batch, head) and walks its key blocks in order, so a query slice's dQ is summed in registers
 // within a key block and across key blocks through plain fp32 stores/loads of the same lanes (L2
-// resident, no atomics, deterministic); the last contributing key block writes dQ (bf16, RoPE-inverse
-// fused). With B·H >> 256 CUs the grid still fills the chip (XL: 1200 workgroups, ~4.7 per CU).
+// resident, no atomics, deterministic); the last contributing key block writes dQ (bf16). RoPE, if any, is undone by one
+// pass over d(q|k) after this kernel (csrc/bindings.cpp fa_bwd_run): measured faster than a rotating
+// store here. With B·H >> 256 CUs the grid still fills the chip (XL: 1200 workgroups, ~4.7 per CU).
 //
 // Structure (cdna_hip_programming.md "Attention backward"): 8 waves, two per SIMD (≤ 256 registers
 // each); key block = 256 keys; wave w owns the 32-key group g = w (w < 4) or 11 - w, so the two
@@ -52,7 +53,7 @@ constexpr int FLDS = OFF_D + FMAXN * 4;
 static_assert(FLDS <= 160 * 1024, "LDS budget");
 }  // namespace
 
-template <typename T, bool CAUSAL, int ROPE>
+template <typename T, bool CAUSAL>
 __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParams bp) {
   typedef typename Elem<T>::storage S;
   typedef typename Mma16<T>::frag F;
@@ -181,19 +182,15 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
   auto store_kv = [&](int kb) {
     const int key = kb * FKB + 32 * g + l32;
     if (key >= N) return;
-    const int64_t kpos = bp.f.rope_pos ? bp.f.rope_pos[(int64_t)b * N + key] : key;
     S* rk = (S*)bp.dk + b * bp.dk_sb + h * bp.dk_sh + key * dk_sn;
     S* rv = (S*)bp.dv + b * bp.dv_sb + h * bp.dv_sh + key * dv_sn;
-    const Rope rope{bp.f.rope_cos, bp.f.rope_sin, FD / 2};
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int d = 32 * dt + 8 * g4 + 4 * hh;
-        float v0 = dk[dt][4 * g4] * sc, v1 = dk[dt][4 * g4 + 1] * sc, v2 = dk[dt][4 * g4 + 2] * sc,
-              v3 = dk[dt][4 * g4 + 3] * sc;
-        if (ROPE != 0) rope_inv4(v0, v1, v2, v3, rope, kpos, d);  // dK w.r.t. the un-rotated k
-        store4<T>(rk + d, make_float4(v0, v1, v2, v3));
+        store4<T>(rk + d, make_float4(dk[dt][4 * g4] * sc, dk[dt][4 * g4 + 1] * sc, dk[dt][4 * g4 + 2] * sc,
+                                      dk[dt][4 * g4 + 3] * sc));
         store4<T>(rv + d, make_float4(dv[dt][4 * g4], dv[dt][4 * g4 + 1], dv[dt][4 * g4 + 2], dv[dt][4 * g4 + 3]));
       }
   };
@@ -372,17 +369,8 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
           }
           if (last) {
             const int d = 32 * dqt + 8 * g4 + 4 * hh;
-            v0 *= sc;
-            v1 *= sc;
-            v2 *= sc;
-            v3 *= sc;
-            if (ROPE != 0) {  // dQ w.r.t. the un-rotated q
-              const int64_t qpos = bp.f.rope_pos ? bp.f.rope_pos[(int64_t)b * N + qrow] : qrow;
-              const Rope rope{bp.f.rope_cos, bp.f.rope_sin, FD / 2};
-              rope_inv4(v0, v1, v2, v3, rope, qpos, d);
-            }
             S* dQp = (S*)bp.dq + b * bp.dq_sb + h * bp.dq_sh;
-            store4<T>(dQp + qrow * dq_sn + d, make_float4(v0, v1, v2, v3));
+            store4<T>(dQp + qrow * dq_sn + d, make_float4(v0 * sc, v1 * sc, v2 * sc, v3 * sc));
           } else {
             *reinterpret_cast<float4*>(part + qrow * FD + 8 * g4) = make_float4(v0, v1, v2, v3);
           }
@@ -404,8 +392,7 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
 template <typename T, bool C>
 void launch_fused_c(const AttnBwdParams& bp, hipStream_t s) {
   const dim3 grid((unsigned)(bp.f.B * bp.f.H)), block(512);
-  if (bp.f.rope_cos != nullptr) hipLaunchKernelGGL((fa_bwd_fused_kernel<T, C, 2>), grid, block, 0, s, bp);
-  else hipLaunchKernelGGL((fa_bwd_fused_kernel<T, C, 0>), grid, block, 0, s, bp);
+  hipLaunchKernelGGL((fa_bwd_fused_kernel<T, C>), grid, block, 0, s, bp);
 }
 
 }  // namespace fa
@@ -413,7 +400,7 @@ void launch_fused_c(const AttnBwdParams& bp, hipStream_t s) {
 bool flash_attn_bwd_fused_ok(const AttnBwdParams& bp, DType t) {
   const AttnParams& p = bp.f;
   return t != DType::F32 && p.D == 64 && p.Nq == p.Nk && p.Nq % 64 == 0 && p.Nq > 0 && p.Nq <= fa::FMAXN &&
-         (p.rope_cos == nullptr || p.rope_out_only) && bp.dq_acc != nullptr;
+         p.rope_cos == nullptr && bp.dq_acc != nullptr;
 }
 
 void flash_attn_bwd_fused(const AttnBwdParams& bp, DType t, hipStream_t s) {
