@@ -57,11 +57,13 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="xl")
     ap.add_argument("--ctx", type=int, default=512)
-    # 48 x 512 = 24576 tokens per GPU. Per-GPU batch sweep of the XL step on 1x MI355X
-    # (profiles/r2_batch_sweep.md; scripts/ab.py bench "b24::--batch 24" ...): multiples of 24 run the best hipBLASLt
-    # shapes (24 -> 68.5k, 48 -> 69.4-69.7k, 72 -> 68.9k tok/s; 32/40/64/96 -> 65.2-65.8k); 48 also
-    # doubles the backward that hides each step's 8 GB of gradient all-reduce under DDP, at 116 GiB.
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("CS336_BENCH_BATCH", 48)), help="per-GPU batch")
+    # 96 x 512 = 49152 tokens per GPU (188 GiB of the 288). Per-GPU batch sweep of the XL step on
+    # 1x MI355X with the round-3 kernels (profiles/r3_batch_sweep_s5.md): 48 -> 83.5k, 72 -> 84.3k,
+    # 96 -> 85.9-86.1k tok/s -- the per-step fixed costs (fused AdamW over 2.0 B parameters, the
+    # vocabulary head, launch tails) amortize over twice the tokens, and under DDP the backward that
+    # hides each step's 8 GB gradient all-reduce doubles. (Round 2, hipBLASLt-era sweep:
+    # profiles/r2_batch_sweep.md.) The committed GEMM table and dW plans cover 24576 and 49152 tokens.
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("CS336_BENCH_BATCH", 96)), help="per-GPU batch")
     ap.add_argument("--vocab", type=int, default=10000)
     ap.add_argument(
         "--ddp",

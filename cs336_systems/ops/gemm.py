@@ -428,6 +428,13 @@ DW_PLANS: dict = {
     (24576, 1600, 6400): (True, 2),  # W2: 0.442 (lt 0.60; from dYᵀ 0.43 + its transpose)
     (24576, 4800, 1600): (False, 5),  # QKV: 0.377 (default 0.386)
     (24576, 1600, 1600): (False, 7),  # O: 0.139 (lt 0.224; split-K torch 0.164 + dYᵀ transpose)
+    (24576, 10000, 1600): (False, 5),  # vocabulary head
+    # per-GPU batch 96 (49152 tokens), profiles/r3_gemm8w_bench_49152.json: the same plans win
+    (49152, 12800, 1600): (False, 1),  # W1|W3: 1.574 (lt 2.587)
+    (49152, 1600, 6400): (True, 2),  # W2: 0.821 (lt 1.295)
+    (49152, 4800, 1600): (False, 5),  # QKV: 0.678 (lt 0.950)
+    (49152, 1600, 1600): (False, 7),  # O: 0.254 (lt 0.419)
+    (49152, 10000, 1600): (False, 5),  # vocabulary head: 1.386 (lt 2.147)
 }
 
 

@@ -16,7 +16,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 T = 24576
-PROBLEMS = [("w13 dW", 12800, 1600), ("w2 dW", 1600, 6400), ("qkv dW", 4800, 1600), ("o dW", 1600, 1600)]
+PROBLEMS = [("w13 dW", 12800, 1600), ("w2 dW", 1600, 6400), ("qkv dW", 4800, 1600), ("o dW", 1600, 1600), ("lm dW", 10000, 1600)]
 
 
 def timeit(fn, reps=10):
@@ -33,8 +33,11 @@ def timeit(fn, reps=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
+    ap.add_argument("--tokens", type=int, default=24576)
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
+    global T
+    T = args.tokens
     from cs336_systems import ops
 
     assert ops.load_ext(), ops.load_error()

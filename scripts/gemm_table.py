@@ -2,7 +2,10 @@
 committed selection table ``cs336_systems/tuning/gemm_table_mi355x.json`` (problem key -> pick).
 
     CS336_GEMM_TABLE=0 CS336_GEMM_REPORT=gpurun_out/rep.json python bench.py --steps 3 --warmup 2
-    python scripts/gemm_table.py gpurun_out/rep.json [more reports ...]
+    python scripts/gemm_table.py gpurun_out/rep.json [more reports ...] [--merge]
+
+--merge keeps the committed table's entries for problems the given reports do not cover (e.g. adding
+the shapes of another per-GPU batch).
 
 With several reports (several boxes or runs) each problem takes the candidate with the lowest
 median time over the reports, so one slow box or one noisy timing does not decide it.
@@ -18,6 +21,8 @@ OUT = os.path.join(REPO, "cs336_systems", "tuning", "gemm_table_mi355x.json")
 
 
 def main(paths):
+    merge = "--merge" in paths
+    paths = [p for p in paths if p != "--merge"]
     times: dict[str, dict[str, list[float]]] = {}
     for p in paths:
         for r in json.load(open(p)):
@@ -42,7 +47,15 @@ def main(paths):
         if os.path.exists(p + ".lt.json"):
             pins = json.load(open(p + ".lt.json"))
             break
-    doc = {"_meta": {"sources": [os.path.relpath(p, REPO) for p in paths], "rule": "median ms over reports; blas unless beaten by > 3 %",
+    sources = [os.path.relpath(p, REPO) for p in paths]
+    if merge:  # keep the committed table's other problems, pins and provenance; these reports add or override
+        old = json.load(open(OUT))
+        entries = {**old["entries"], **entries}
+        detail = {**old["_meta"].get("median_ms", {}), **detail}
+        have = {",".join(x.split(",", 6)[:6]) for x in pins}
+        pins = pins + [x for x in old.get("lt_pins", []) if ",".join(x.split(",", 6)[:6]) not in have]
+        sources = old["_meta"].get("sources", []) + sources
+    doc = {"_meta": {"sources": sources, "rule": "median ms over reports; blas unless beaten by > 3 %",
                      "median_ms": detail}, "entries": entries, "lt_pins": pins}
     with open(OUT, "w") as f:
         json.dump(doc, f, indent=1)

@@ -27,6 +27,12 @@ def _run(nproc: int, *extra: str) -> list[dict]:
     return [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
 
 
+def _gpu_visible() -> bool:
+    import torch
+
+    return torch.cuda.device_count() > 0
+
+
 @pytest.mark.parametrize(
     "nproc,extra",
     [(2, ()), (4, ()), (2, ("--sharded",)), (2, ("--ddp", "zero")), (2, ("--grad-comm-dtype", "bf16"))],
@@ -42,7 +48,8 @@ def test_bench_multirank_json(nproc, extra):
     assert d["config"]["global_batch"] == 2 * nproc
     assert d["config"]["parallelism"].startswith(f"dp{nproc}")
     assert d["value"] > 0 and d["ms_per_step"] > 0
-    assert "HIP" not in d["config"]["attention"]  # CPU run must not claim the HIP kernels
+    if not _gpu_visible():
+        assert "HIP" not in d["config"]["attention"]  # CPU run must not claim the HIP kernels
     assert d["value"] == pytest.approx(2 * nproc * 32 / (d["ms_per_step"] / 1e3), rel=0.02)
     # multi-rank diagnostics (the 8-GPU run must be diagnosable from its own line)
     dd = d["dist"]
