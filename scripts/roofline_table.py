@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--ff", type=int, default=6400)
     ap.add_argument("--layers", type=int, default=48)
     ap.add_argument("--heads", type=int, default=25)
-    ap.add_argument("--batch", type=int, default=48)
+    ap.add_argument("--batch", type=int, default=96)  # bench.py default per-GPU batch
     ap.add_argument("--ctx", type=int, default=512)
     ap.add_argument("--vocab", type=int, default=10000)
     a = ap.parse_args()
