@@ -239,6 +239,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
 #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
       if (t < ntiles) issue(t);
+    // the resident Q / dO fragments retired, stated to the compiler (see the dK/dV kernel's prologue)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     auto dstep = [&](int j, auto slot) __attribute__((always_inline)) {
       if (NS == 3 && j + 1 < ntiles) wait_vmcnt<2 * Dma::PER_WAVE>();
       else wait_vmcnt<0>();
@@ -592,6 +594,11 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
 #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
       if (qt_begin + t < qt_end) issue(qt_begin + t);
+    // The resident K / V fragments (loaded above) retired, stated to the compiler: it cannot see the
+    // inline-asm DMA or the counted asm waits, so without this it keeps them pending and puts
+    // vmcnt(0/1) in front of their first MFMA in EVERY tile -- a drain of the prefetch ring per tile.
+    // Costs one wait for the prologue's DMA, which the first tile waits for anyway.
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     auto dstep = [&](int it, auto slot, auto mask_tag) __attribute__((always_inline)) {
       if (NS == 3 && it + 1 < qt_end) wait_vmcnt<PER_TILE>();
       else wait_vmcnt<0>();

@@ -312,6 +312,12 @@ struct TileDma {
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  // A full drain is also stated to the compiler (vmcnt 0; expcnt / lgkmcnt left at their maxima),
+  // which cannot see the inline-asm wait above: otherwise operands it loaded earlier (the V / K / Q
+  // fragments kept in registers) count as pending forever after, and it re-inserts vmcnt(0) in
+  // front of their MFMAs inside the tile loop -- a drain of the LDS-DMA prefetch (invisible to it)
+  // at every tile. At runtime this adds nothing: the counter is already 0.
+  if constexpr (N == 0) __builtin_amdgcn_s_waitcnt(0x0F70);
 }
 
 // Workgroup barrier that keeps LDS-DMA in flight: __syncthreads()'s fence makes hipcc emit

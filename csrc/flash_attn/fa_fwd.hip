@@ -266,6 +266,7 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
       issue_v(t);
     }
     issue_k(NS - 1);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // resident Q retired, stated to the compiler (see above)
     wait_vmcnt<(2 * NS - 2) * PW>();  // K(0) landed
     dma_barrier();
     f32x16 sa[2], sb[2];
@@ -312,6 +313,9 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
 #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
       if (t < ntiles) issue(t);
+    // the resident Q fragments retired, stated to the compiler, which cannot see the inline-asm DMA
+    // or the counted asm waits (else it re-waits vmcnt(0) before their MFMAs in every tile)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     auto step = [&](int j, auto slot) __attribute__((always_inline)) {
       // this wave's pieces of tile j have landed once only the younger tiles' DMAs are in flight;
       // the barrier then publishes every wave's pieces and retires all reads of tile j-1's slot
