@@ -97,7 +97,9 @@ void fill_attn(cs336::AttnParams& p, const at::Tensor& q, const at::Tensor& k, c
   // backward (bit 2): with the dQ / dK-dV DMA loops unrolled by their ring depth LDS-DMA staging
   // wins at Nk >= 1024 (d 64 +5 %, d 128 +5-10 %, d 80 even); it loses 2 % at the XL step's N 512
   // (profiles/r2_fa_bwd_valu.md)
-  if (dma_env < 0) p.dma = ((!causal || p.D >= 128 || p.Nk >= 1024) ? 1 : 0) | (p.Nk >= 1024 ? 2 : 0);
+  // (since the resident-fragment wait hint, profiles/r3_fa_vmcnt_hint.md, the LDS-DMA forward also
+  // wins at the XL step's causal N 512: 0.1306-0.1313 vs 0.1343-0.1357 ms, so it is every forward)
+  if (dma_env < 0) p.dma = 1 | (p.Nk >= 1024 ? 2 : 0);
   else if (dma_env == 4) p.dma = 1 | 4;
   else p.dma = dma_env == 0 ? 0 : (dma_env == 1 ? 1 : 3);
 }
