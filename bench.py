@@ -111,6 +111,14 @@ def parse(argv=None):
         help="N > 1: after the timed steps, fp32 all-reduce sweep (5 warmup + 5 timed each) added to the JSON's dist block",
     )
     ap.add_argument(
+        "--ddp-sweep",
+        default="auto",
+        choices=["auto", "on", "off"],
+        help="N > 1 (auto): after the timed steps, the handout's DDP comparison -- naive / flat / per-parameter / "
+        "bucketed {1,10,100,1000} MB ms/step + comm wait, ZeRO-1 memory -- into the JSON's dist block (<= 60 s)",
+    )
+    ap.add_argument("--ddp-sweep-batch", type=int, default=4, help="per-GPU batch of the DDP sweep")
+    ap.add_argument(
         "--tunableop",
         default="auto",
         choices=["auto", "off", "use", "tune"],
@@ -207,6 +215,12 @@ def dist_diagnostics(ddp_model, comm_wait_ms, device, world) -> dict:
     d["env"] = {k: v for k, v in sorted(os.environ.items())
                 if k.startswith(("NCCL_", "RCCL_", "HSA_", "TORCH_NCCL_", "TENSILE_STREAMK"))}
     d["coresidency_caps"] = dict(_CORES_ENV)
+    # per-rank CPU affinity (each rank pinned to its GPU's NUMA-local CPUs in setup_distributed)
+    from cs336_systems.parallel.affinity import affinity_info
+
+    per_rank: list = [None] * dist.get_world_size()
+    dist.all_gather_object(per_rank, {"rank": dist.get_rank(), **affinity_info()})
+    d["cpu_affinity"] = per_rank
     if buckets and world > 1 and device.type == "cuda" and dist.get_backend() == "nccl":
         n = int(max(mbs) * 2**20 // 4)
         buf = torch.ones(n, dtype=torch.float32, device=device)
@@ -440,6 +454,20 @@ def main(argv=None):
         out["dist"] = dist_diagnostics(ddp_model, comm_wait_ms, device, world)
         if world > 1 and args.comm_sweep_mb:
             out["dist"]["allreduce_sweep_fp32"] = comm_sweep(args.comm_sweep_mb, device, world)
+    if world > 1 and args.ddp_sweep != "off" and not zero:
+        # the headline fields are final; free the timed model, then the bounded DDP-variant table
+        del ddp_model, opt, model, batches, graphed
+        if device.type == "cuda":
+            torch.cuda.empty_cache()
+        from cs336_systems.bench.ddp import sweep_variants
+
+        try:
+            sw = sweep_variants(args.model, args.ctx, args.ddp_sweep_batch, device, amp=amp, vocab=args.vocab)
+            out["dist"]["ddp_variants"] = sw.pop("variants")
+            out["dist"]["zero1_memory"] = sw.pop("zero1_memory")
+            out["dist"]["ddp_sweep"] = sw
+        except Exception as e:  # noqa: BLE001 - the sweep never costs the headline line
+            out["dist"]["ddp_sweep"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if tmode == "tune" and rank == 0:
         import torch.cuda.tunable as tunable
 

@@ -164,6 +164,109 @@ def train_ddp(rank: int, world: int, args) -> dict | None:
     return out
 
 
+SWEEP_VARIANTS = (("naive", None), ("flat", None), ("individual", None), ("bucketed", 1.0), ("bucketed", 10.0),
+                  ("bucketed", 100.0), ("bucketed", 1000.0))
+
+
+def sweep_variants(model_name: str, ctx: int, per_rank_batch: int, dev: torch.device, *, steps: int = 2,
+                   warmup: int = 1, amp: bool = True, vocab: int = 10000, budget_s: float = 60.0,
+                   variants=SWEEP_VARIANTS, zero1: bool = True) -> dict:
+    """The handout's multi-GPU DDP comparison on an already-initialised process group (reference
+    ``naive_ddp.py:269-442, 444-634``; ``ddp_bucketed_overlapped_sharded.py:131-214, 366-419``;
+    handout p.27-31, p.34-35): per variant (naive, flat, per-parameter, bucketed at each bucket
+    size) ``warmup`` + ``steps`` full steps of a fresh model at ``per_rank_batch`` sequences per rank,
+    reporting ms/step and the exposed gradient-communication wait (max over ranks); then ZeRO-1
+    (:class:`ShardedOptimizer` over bucketed DDP) memory after init / peak before / after the
+    optimizer step. Stops issuing new variants once ``budget_s`` of wall time is spent (the rest are
+    reported as skipped); every rank takes the same decisions (rank 0's clock is broadcast)."""
+    t_start = time.perf_counter()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    rows, mem = [], None
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(4321 + rank)
+    autocast = (lambda: torch.autocast(dev.type, dtype=torch.bfloat16)) if amp else contextlib.nullcontext
+
+    def over_budget() -> bool:
+        t = torch.tensor([time.perf_counter() - t_start], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.broadcast(t, 0)
+        return float(t.item()) > budget_s
+
+    def run(variant, bucket_mb, sharded=False):
+        torch.manual_seed(1234)
+        model = build_model(model_name, ctx, vocab_size=vocab, device=dev)
+        shadows = amp and dev.type == "cuda"
+        if dev.type == "cuda":
+            torch.cuda.reset_peak_memory_stats(dev)
+        ddp = wrap_ddp(model, variant, bucket_size_mb=bucket_mb)
+        okw = dict(lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01)
+        if sharded:
+            opt = ShardedOptimizer(model.parameters(), ops.FusedAdamW, bf16_shadows=shadows, **okw).attach(ddp)
+        else:
+            opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)
+        _sync(dev)
+        mem_init = _mem(dev)
+        x, y = synthetic_batch(per_rank_batch, ctx, vocab, dev, gen)
+        step_ms, comm_ms, before, after = [], [], [], []
+        for it in range(warmup + steps):
+            _sync(dev)
+            t0 = time.perf_counter()
+            opt.zero_grad(set_to_none=True)
+            with autocast():
+                loss = ops.cross_entropy(ddp(x), y)
+            loss.backward()
+            _sync(dev)
+            t1 = time.perf_counter()
+            ddp.finish_gradient_synchronization()
+            _sync(dev)
+            t2 = time.perf_counter()
+            before.append(_peak(dev))
+            opt.step()
+            _sync(dev)
+            t3 = time.perf_counter()
+            after.append(_peak(dev))
+            if it >= warmup:
+                step_ms.append((t3 - t0) * 1e3)
+                comm_ms.append((t2 - t1) * 1e3)
+        t = torch.tensor([statistics.fmean(step_ms), statistics.fmean(comm_ms), mem_init, max(before), max(after)],
+                         dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        del ddp, opt, model, loss
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        return [float(v) for v in t.tolist()]
+
+    for variant, bucket_mb in variants:
+        row = {"variant": variant, "bucket_mb": bucket_mb}
+        if over_budget():
+            row["skipped"] = "time budget"
+        else:
+            try:
+                st, cw, *_ = run(variant, bucket_mb)
+                row.update(ms_per_step=round(st, 3), comm_wait_ms=round(cw, 3),
+                           comm_fraction=round(cw / st, 4) if st else 0.0)
+            except Exception as e:  # noqa: BLE001 - reported in the JSON, never loses the headline
+                row["error"] = f"{type(e).__name__}: {e}"[:300]
+        rows.append(row)
+    if zero1:
+        if over_budget():
+            mem = {"skipped": "time budget"}
+        else:
+            try:
+                _, _, m0, mb, ma = run("bucketed", DEFAULT_BUCKET_MB, sharded=True)
+                _, _, r0, rb, ra = run("bucketed", DEFAULT_BUCKET_MB, sharded=False)
+                mem = {"zero1": {"after_init_mib": round(m0, 1), "peak_before_step_mib": round(mb, 1),
+                                 "peak_after_step_mib": round(ma, 1)},
+                       "replicated": {"after_init_mib": round(r0, 1), "peak_before_step_mib": round(rb, 1),
+                                      "peak_after_step_mib": round(ra, 1)},
+                       "bucket_mb": DEFAULT_BUCKET_MB}
+            except Exception as e:  # noqa: BLE001
+                mem = {"error": f"{type(e).__name__}: {e}"[:300]}
+    return {"model": model_name, "ctx": ctx, "per_rank_batch": per_rank_batch, "steps": steps, "warmup": warmup,
+            "world": world, "variants": rows, "zero1_memory": mem,
+            "wall_s": round(time.perf_counter() - t_start, 2)}
+
+
 def _spawned(rank, world, args):
     train_ddp(rank, world, args)
 

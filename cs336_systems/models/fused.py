@@ -301,9 +301,9 @@ def compute_weight(params: list[nn.Parameter], dtype: torch.dtype) -> torch.Tens
 # this stream. hipBLASLt has no data-parallel alternative for these problems on gfx950 (2198 of
 # its 2199 solutions are stream-K, scripts/lt_dp_probe.py), so a weight gradient goes to the side
 # stream only if the cs336 MFMA GEMM (whole tiles per workgroup, no inter-workgroup waits) takes it
-# (gemm.dw_concurrent_ok); otherwise it runs on the main stream. A GEMM
-# beside a bounded occupant such as an RCCL kernel (which ends when its peers arrive) only waits
-# for it, it cannot deadlock (tests/test_concurrency_gpu.py).
+# (gemm.dw_concurrent_ok); otherwise it runs on the main stream. A cs336 GEMM beside an RCCL
+# kernel only waits for it (tests/test_concurrency_gpu.py); a stream-K grid beside RCCL is the
+# hazard cs336_systems/rccl_env.py caps (profiles/r3_coresidency.md).
 _SIDE_STREAMS: dict[int, torch.cuda.Stream] = {}
 _state = {"dirty": False, "callback": False}
 
@@ -680,20 +680,23 @@ class QKVRopeLinearFn(torch.autograd.Function):
         sub.mm_override = mm
         y = FusedLinearFn.forward(sub, x, None, *weights)
         ctx.sub = sub
+        _stash_saved(ctx, sub)
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        _unstash_saved(ctx, ctx.sub)
         dx, _, *dws = FusedLinearFn.backward(ctx.sub, dy)
         ctx.sub._saved = ()
-        ctx.sub = None
         return (dx, None, None, None, None, *dws)
 
 
 class _SubCtx:
     """Stand-in for an autograd ctx, so FusedLinearFn's forward/backward run as one stage of a
     larger Function (SwiGLUFFNFn) and keep all their logic: bf16/Wᵀ shadows, Xᵀ / dYᵀ layouts,
-    fp32 dW written straight into the DDP bucket."""
+    fp32 dW written straight into the DDP bucket. The outer Function hands the stage's tensors to
+    its own ``ctx.save_for_backward`` (:func:`_stash_saved`), so they get autograd's version-counter
+    check, ``saved_tensors_hooks`` (checkpointing / offload) and ``retain_graph`` semantics."""
 
     def __init__(self, needs_input_grad):
         self.needs_input_grad = tuple(needs_input_grad)
@@ -705,6 +708,26 @@ class _SubCtx:
     @property
     def saved_tensors(self):
         return self._saved
+
+
+def _stash_saved(ctx, *subs, extra: tuple = ()) -> None:
+    """Save the stages' tensors (then ``extra``) through the outer ``ctx.save_for_backward``; the
+    stages keep only their counts (plain attributes bypassed version checks and hooks)."""
+    ctx.sub_counts = [len(sub._saved) for sub in subs]
+    ctx.save_for_backward(*[t for sub in subs for t in sub._saved], *extra)
+    for sub in subs:
+        sub._saved = ()
+
+
+def _unstash_saved(ctx, *subs) -> tuple:
+    """Give each stage back its saved tensors (version-checked by ``ctx.saved_tensors``); returns
+    the ``extra`` tensors."""
+    ts = ctx.saved_tensors
+    i = 0
+    for sub, n in zip(subs, ctx.sub_counts):
+        sub._saved = tuple(ts[i : i + n])
+        i += n
+    return tuple(ts[i:])
 
 
 def swiglu_fused_enabled() -> bool:
@@ -745,13 +768,13 @@ class SwiGLUFFNFn(torch.autograd.Function):
         c2 = _SubCtx((True, False, w2.requires_grad))
         out = FusedLinearFn.forward(c2, h, None, w2)
         ctx.c13, ctx.c2 = c13, c2
-        ctx.save_for_backward(y)
+        _stash_saved(ctx, c13, c2, extra=(y,))
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        (y,) = ctx.saved_tensors
         c13, c2 = ctx.c13, ctx.c2
+        (y,) = _unstash_saved(ctx, c13, c2)
         c2.skip_dx = True  # W2 stage: weight gradient only; its input gradient is fused below
         _, _, dw2 = FusedLinearFn.backward(c2, dout)
         h2, w2s = c2.saved_tensors
@@ -770,10 +793,9 @@ class SwiGLUFFNFn(torch.autograd.Function):
             dh = gemm.mm_nt(dy2, w2s) if c2.w_t else gemm.mm_nn(dy2, w2s)
             dab = _hip().swiglu_fused_bwd(dh.contiguous(), y2)
         dx, _, dw1, dw3 = FusedLinearFn.backward(c13, dab.view(*y.shape))
-        # the stages' saved tensors are plain attributes (not SavedVariables): drop them now, or
-        # every layer's h / Xᵀ would live until the whole graph is freed (+18 GiB peak on XL)
+        # drop the stages' references now (autograd frees its SavedVariables after this backward
+        # unless retain_graph; a stage reference would keep every layer's h / X alive: +18 GiB on XL)
         c13._saved = c2._saved = ()
-        ctx.c13 = ctx.c2 = None
         return dx, dw1, dw3, dw2
 
 

@@ -130,6 +130,12 @@ def _pick(kind: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None,
             _BEST[key] = "blas"
             _BEST_TIMES[key] = {"untimed_multi_rank": "blas"}
             return "blas"
+        # the partials of a split-K candidate are extra memory at the selection step (first step,
+        # inside backward): time one only with room to spare; free memory is queried
+        # here, on a cache miss, not on every call
+        if any(hasattr(fn, "partial_bytes") for fn in cands.values()):
+            free = torch.cuda.mem_get_info()[0]
+            cands = {n: fn for n, fn in cands.items() if getattr(fn, "partial_bytes", 0) + (4 << 30) <= free}
         times = {name: _time_ms(fn) for name, fn in cands.items()}
         best = min(times, key=times.get)
         hit = _BEST[key] = best if times[best] < 0.97 * times["blas"] else "blas"
@@ -184,9 +190,20 @@ def _aligned_rows(t: torch.Tensor) -> bool:
     return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0
 
 
+DMA_LIMIT = (1 << 31) - (1 << 20)  # gemm8 / gemm8w: one buffer descriptor per operand, 32-bit offsets
+
+
+def gemm8_extents_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Both operand extents the gemm8 kernel addresses (256 rows of ``x``, all rows of ``w``) fit
+    its 2 GiB DMA range (mirrors ``gemm8_extents_ok`` in csrc/bindings.cpp)."""
+    k = x.shape[1]
+    return (255 * x.stride(0) + k) * 2 < DMA_LIMIT and ((w.shape[0] - 1) * w.stride(0) + k) * 2 < DMA_LIMIT
+
+
 def gemm8_ok(x: torch.Tensor, w: torch.Tensor, epi: int = 0, half: int = 0) -> bool:
     """Whether the gemm8 NT kernel (``csrc/gemm/gemm8.hip``) takes ``x @ w.T``: bf16, row-major with
-    16-B aligned rows, M % 256, K % 64, N a multiple of 320 or 256 (epi 1: half of 160 or 128)."""
+    16-B aligned rows, M % 256; epi 0: N and K multiples of 8 (partial last tiles masked); epi 1-3:
+    K % 64, N a multiple of 320 or 256 (epi 1: half of 160 or 128); operand extents < 2 GiB."""
     return (
         x.is_cuda
         and x.dtype == torch.bfloat16
@@ -196,6 +213,7 @@ def gemm8_ok(x: torch.Tensor, w: torch.Tensor, epi: int = 0, half: int = 0) -> b
         and x.shape[1] == w.shape[1]
         and ext_available()
         and ops().gemm8_ok(x.shape[0], w.shape[0], x.shape[1], epi, half)
+        and gemm8_extents_ok(x, w)
     )
 
 
@@ -327,19 +345,15 @@ def _splitk_cands(a3_of, b3_of, k: int, m: int, n: int, out: torch.Tensor | None
     if m * n > int(os.environ.get("CS336_SPLITK_MAX_OUT", SPLITK_MAX_OUT)) or os.environ.get("CS336_SPLITK", "1") == "0":
         return {}
     res = {}
-    # the partials of the candidate being timed are extra memory at the selection step (first
-    # step, inside backward): time a candidate only with room to spare
-    free = torch.cuda.mem_get_info()[0] if torch.cuda.is_available() else 0
     for sk in (2, 4, 8):
         if k % sk or (k // sk) % 64 or sk * m * n * 4 > SPLITK_MAX_PARTIAL_BYTES:
-            continue
-        if sk * m * n * 4 + (4 << 30) > free:
             continue
 
         def run(sk=sk):
             part = torch.bmm(a3_of(sk), b3_of(sk), out_dtype=torch.float32)
             return torch.sum(part, dim=0, out=out) if out is not None else part.sum(0)
 
+        run.partial_bytes = sk * m * n * 4  # checked against free memory before it is timed (_pick)
         res[f"splitk{sk}"] = run
     return res
 
@@ -465,6 +479,24 @@ def _dw_plan(T: int, n_out: int, k_in: int) -> tuple[bool, int] | None:
     return best
 
 
+def g8w_split_fits(T: int, sk: int, dy: torch.Tensor, x: torch.Tensor) -> bool:
+    """One gemm8w split's operand extent (its token rows x the wider row stride) fits the kernel's
+    2 GiB DMA range (csrc/bindings.cpp ``gemm8w``); a single split is cut into token chunks there."""
+    rows = -(-(T // 64) // sk) * 64
+    return rows * max(dy.stride(0), x.stride(0)) * 2 + max(dy.shape[1], x.shape[1]) * 2 < DMA_LIMIT
+
+
+def dw_launch_plan(dy: torch.Tensor, x: torch.Tensor) -> tuple[bool, int]:
+    """(transposed roles, splits) that :func:`mm_dw` launches: the measured / modelled plan, except
+    that a split past the 2 GiB DMA range becomes one split, which the binding cuts into token
+    chunks accumulated in place (e.g. a 50304-vocabulary head at 49152 tokens: 4.9 GB of dY)."""
+    T = dy.shape[0]
+    trans, sk = _dw_plan(T, dy.shape[1], x.shape[1])
+    if sk > 1 and not g8w_split_fits(T, sk, dy, x):
+        sk = 1
+    return trans, sk
+
+
 def dw_g8w_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
     return (dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.dim() == 2 and x.dim() == 2
             and dy.shape[0] == x.shape[0] and _aligned_rows(dy) and _aligned_rows(x) and dy.shape[0] % 64 == 0
@@ -475,15 +507,19 @@ def mm_dw(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None, ac
     """``dy.T @ x`` with an fp32 result from token-major ``dy`` (T, N_out) and ``x`` (T, K_in) --
     written into ``out`` (e.g. a DDP bucket view; ``accumulate``: added to it) when given."""
     T, n_out, k_in = dy.shape[0], dy.shape[1], x.shape[1]
-    trans, sk = _dw_plan(T, n_out, k_in)
+    trans, sk = dw_launch_plan(dy, x)
     a, b = (x, dy) if trans else (dy, x)
     if out is None:
         out = torch.empty(n_out, k_in, device=dy.device, dtype=torch.float32)
         accumulate = False
-    direct = sk == 1 and out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0
-    if direct:
-        ops().gemm8w(a, b, out, 1, trans, accumulate, 0)
-        return out
+    direct = out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0
+    if sk == 1:
+        if direct:
+            ops().gemm8w(a, b, out, 1, trans, accumulate, 0)
+            return out
+        tmp = torch.empty(n_out, k_in, device=dy.device, dtype=torch.float32)
+        ops().gemm8w(a, b, tmp, 1, trans, False, 0)
+        return out.add_(tmp) if accumulate else out.copy_(tmp)
     slabs = torch.empty(sk, n_out, k_in, device=dy.device, dtype=torch.float32)
     ops().gemm8w(a, b, slabs, sk, trans, False, 0)
     if accumulate:

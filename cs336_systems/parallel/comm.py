@@ -22,6 +22,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from .affinity import pin_rank_to_gpu
+
 
 def find_free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -66,6 +68,8 @@ def setup_distributed(
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
+    # host threads of this rank on the CPUs local to its GPU, before any heavy host work
+    pin_rank_to_gpu(dev)
     if not dist.is_initialized():
         kw = {}
         if backend == "nccl" and dev.type == "cuda":

@@ -44,11 +44,17 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
+from .rccl_env import apply_multi_gpu_env
 
-from . import ops
+# co-residency caps for multi-rank runs (stream-K grid cap, RCCL channel cap), set before torch loads
+# hipBLASLt / RCCL, exactly as bench.py does
+_CORES_ENV = apply_multi_gpu_env(int(os.environ.get("WORLD_SIZE", "1")))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from . import ops  # noqa: E402
 from .checkpoint import latest_checkpoint, load_checkpoint, load_optimizer_state, save_checkpoint
 from .models import build_model
 from .models.fused import refresh_bf16_shadows

@@ -856,10 +856,20 @@ bool gemm8_check(const at::Tensor& t, int64_t rows, int64_t cols, const char* wh
 
 // epi 3: `half` carries rope_cols, which must cover whole column tiles (the rotation is decided per
 // tile); the binding also needs d_head <= 96 (the tile rows' cos/sin fit the LDS behind the scratch)
+// epi 0 also takes N and K tails (multiples of 8: the vocabulary head, 10000 = 31·320 + 80)
 bool gemm8_ok(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t half) {
+  if (M <= 0 || N <= 0 || K <= 0 || M >= (1 << 30) || N >= (1 << 30) || K >= (1 << 30)) return false;
   const int fn = cs336::gemm8::pick_fn((int)N, (int)epi, (int)half);
-  return fn != 0 && M % 256 == 0 && K % 64 == 0 && K >= 64 && N % (64 * fn) == 0 && M < (1 << 30) &&
-         (epi != 3 || half % (64 * fn) == 0);
+  if (fn == 0 || M % 256) return false;
+  if (epi == 0) return N % 8 == 0 && K % 8 == 0;
+  return K % 64 == 0 && N % (64 * fn) == 0 && (epi != 3 || half % (64 * fn) == 0);
+}
+
+// gemm8 / gemm8w address each operand through one buffer descriptor with 32-bit byte offsets
+constexpr int64_t kDmaLimit = (int64_t(1) << 31) - (int64_t(1) << 20);
+bool gemm8_extents_ok(const at::Tensor& a, const at::Tensor& b) {
+  const int64_t K = a.size(1);
+  return (255 * a.stride(0) + K) * 2 < kDmaLimit && ((b.size(0) - 1) * b.stride(0) + K) * 2 < kDmaLimit;
 }
 
 void gemm8(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, int64_t epi, int64_t fn, const OptT& h,
@@ -869,6 +879,7 @@ void gemm8(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, int64_t epi,
   gemm8_check(b, N, K, "b");
   TORCH_CHECK(epi >= 0 && epi <= 2, "cs336: gemm8 epi");
   TORCH_CHECK(gemm8_ok(M, N, K, epi, half), "cs336: gemm8 does not take M=", M, " N=", N, " K=", K, " epi=", epi);
+  TORCH_CHECK(gemm8_extents_ok(a, b), "cs336: gemm8 operand extent exceeds the 2 GiB DMA range");
   cs336::gemm8::Args p{};
   p.a = reinterpret_cast<const uint16_t*>(a.data_ptr());
   p.b = reinterpret_cast<const uint16_t*>(b.data_ptr());
@@ -911,6 +922,7 @@ void gemm8_rope(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const a
   gemm8_check(c, M, N, "c");
   TORCH_CHECK(gemm8_ok(M, N, K, 3, rope_cols), "cs336: gemm8_rope does not take M=", M, " N=", N, " K=", K,
               " rope_cols=", rope_cols);
+  TORCH_CHECK(gemm8_extents_ok(a, b), "cs336: gemm8_rope operand extent exceeds the 2 GiB DMA range");
   TORCH_CHECK(dhead % 8 == 0 && dhead > 0 && dhead <= 96 && rope_cols % dhead == 0 && rope_cols <= N && seq > 0,
               "cs336: gemm8_rope needs d_head % 8 == 0, d_head <= 96 and whole rotated heads");
   TORCH_CHECK(cos.is_cuda() && sin.is_cuda() && cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat &&
@@ -970,25 +982,40 @@ void gemm8w(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, int64_t s
                     out.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
                 "cs336: gemm8w out shape/alignment");
   }
-  cs336::gemm8::WArgs p{};
-  p.a = reinterpret_cast<const uint16_t*>(a.data_ptr());
-  p.b = reinterpret_cast<const uint16_t*>(b.data_ptr());
-  p.c = out.data_ptr<float>();
-  p.lda = a.stride(0);
-  p.ldb = b.stride(0);
-  p.ldc = splits > 1 ? cols : out.stride(0);
-  p.slab_stride = splits > 1 ? rows * cols : 0;
-  p.a_elems = (K - 1) * a.stride(0) + M;
-  p.b_elems = (K - 1) * b.stride(0) + N;
-  p.M = (int)M;
-  p.N = (int)N;
-  p.K = (int)K;
-  p.splits = (int)splits;
-  p.trans_out = trans_out ? 1 : 0;
-  p.accumulate = accumulate ? 1 : 0;
+  // The kernel addresses one split's token rows through a buffer descriptor with 32-bit byte offsets:
+  // each launch's per-split extent must stay below 2 GiB (a 50304-vocabulary head at
+  // 49152 tokens is 4.9 GB of dY). splits == 1 is cut into token chunks here, each chunk after the
+  // first accumulating into `out`; with split-K slabs the caller must pick enough splits.
+  TORCH_CHECK(K % 64 == 0 && K > 0, "cs336: gemm8w needs K % 64 == 0");
+  const int64_t ld = std::max(a.stride(0), b.stride(0)), wide = std::max(M, N);
+  auto extent = [&](int64_t rows) { return rows * ld * 2 + wide * 2; };
+  const int64_t nkt = K / 64, per_split = (nkt + splits - 1) / splits * 64;
+  TORCH_CHECK(splits == 1 || extent(per_split) < kDmaLimit, "cs336: gemm8w split of ", per_split,
+              " token rows exceeds the 2 GiB DMA range; use more splits (", splits, " given)");
+  const int64_t chunk = std::max<int64_t>(64, std::min(K, (kDmaLimit - wide * 2) / (ld * 2) / 64 * 64));
+  TORCH_CHECK(splits > 1 || extent(chunk) < kDmaLimit, "cs336: gemm8w rows too wide for the DMA range");
   c10::DeviceGuard g(a.device());
-  TORCH_CHECK(cs336::gemm8::launch_w(p, (int)fn, stream()), "cs336: gemm8w does not take M=", M, " N=", N, " K=", K,
-              " splits=", splits);
+  for (int64_t k0 = 0; k0 < K; k0 += (splits > 1 ? K : chunk)) {
+    const int64_t kc = splits > 1 ? K : std::min(chunk, K - k0);
+    cs336::gemm8::WArgs p{};
+    p.a = reinterpret_cast<const uint16_t*>(a.data_ptr()) + k0 * a.stride(0);
+    p.b = reinterpret_cast<const uint16_t*>(b.data_ptr()) + k0 * b.stride(0);
+    p.c = out.data_ptr<float>();
+    p.lda = a.stride(0);
+    p.ldb = b.stride(0);
+    p.ldc = splits > 1 ? cols : out.stride(0);
+    p.slab_stride = splits > 1 ? rows * cols : 0;
+    p.a_elems = (kc - 1) * a.stride(0) + M;
+    p.b_elems = (kc - 1) * b.stride(0) + N;
+    p.M = (int)M;
+    p.N = (int)N;
+    p.K = (int)kc;
+    p.splits = (int)splits;
+    p.trans_out = trans_out ? 1 : 0;
+    p.accumulate = (accumulate || k0 > 0) ? 1 : 0;
+    TORCH_CHECK(cs336::gemm8::launch_w(p, (int)fn, stream()), "cs336: gemm8w does not take M=", M, " N=", N,
+                " K=", kc, " splits=", splits);
+  }
 }
 
 TORCH_LIBRARY(cs336, m) {

@@ -14,6 +14,11 @@
 //          columns below rope_cols (q|k heads) in the store -- no separate RoPE pass over q|k. The
 //          rotation reads the bf16-rounded product, as the separate pass did (same rounding points).
 //
+// Tails (EPI 0 only): N % 8 == 0 with a partial last column tile, K % 8 == 0 with a partial last
+// k-tile -- the vocabulary head's forward (N = 10000) and input gradient (K = 10000), so no hipBLASLt
+// kernel is left in the step. Out-of-range B rows and K chunks are loaded as zeros by the buffer
+// range check; partial-tile stores are masked per 8-column piece.
+//
 // Structure (cdna_hip_programming.md §5 "256² 8-phase template", re-derived for these shapes):
 // * tile 256 × BN (BN = 64·FN: 256 or 320 -- every N of the XL/2.7b projections is a multiple of
 //   320 or 256, d_model 1600 = 5·320), BK = 64, 512 threads = 8 waves as 2 (M) × 4 (N), each wave
@@ -99,7 +104,9 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   const int wr = wave >> 2, wc = wave & 3;
 
   // ---- tile coordinates -------------------------------------------------------------------
-  const int tiles_n = p.N / BN;  // EPI 1: N = 2·half, BN/2 units of each half per tile
+  // EPI 1: N = 2·half, BN/2 units of each half per tile. EPI 0 also takes an N tail (N % BN != 0,
+  // N % 8 == 0: the vocabulary head, 10000 = 31·320 + 80): B rows >= N read zeros, stores masked
+  const int tiles_n = EPI == 0 ? (p.N + BN - 1) / BN : p.N / BN;
   const int tiles_m = p.M / BM;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int per_group = kGroupM * tiles_n;
@@ -111,17 +118,25 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   const int n0 = tn * (EPI == 1 ? BN / 2 : BN);
 
   // ---- DMA setup: per wave G_ALL granules; slot order P1 (A0 then B0), P2 (B1), P3 (A1) ------
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.a + (int64_t)m0 * p.lda), (short)0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, 0x7fffffff, 0x00020000);
+  // The record counts end at each operand's last element (host: both extents < 2 GiB), so B rows
+  // past N (EPI 0 N tail) and the lanes of a K tail pointed at kOOB read zeros (raw-buffer range check)
+  const int nkt = (p.K + BK - 1) / BK;
+  const bool ktail = (p.K % BK) != 0;  // last k-tile partial (K % 8 == 0): its chunks >= K are zero
+  constexpr uint32_t kOOB = 0x7ffffff0u;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.a + (int64_t)m0 * p.lda), (short)0, (uint32_t)(((BM - 1) * p.lda + p.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.b, (short)0, (uint32_t)(((int64_t)(p.N - 1) * p.ldb + p.K) * 2), 0x00020000);
   uint32_t voff[G::G_ALL];   // per-lane byte offset at k-tile 0
   uint32_t ldso[G::G_ALL];   // wave-uniform LDS byte offset within a stage
+  uint32_t tmask = 0;        // granules whose chunk lies past K in the last k-tile
   {
     int s = 0;
     auto a_gran = [&](int row0) {  // A image rows row0..row0+7
       const int r = row0 + (lane >> 3), lc = (lane & 7) ^ ((r >> 1) & 7);
       voff[s] = 2u * (uint32_t)(r * p.lda + lc * 8);
       ldso[s] = (uint32_t)(row0 * 128);
+      if ((nkt - 1) * BK + lc * 8 >= p.K) tmask |= 1u << s;
       ++s;
     };
     auto b_gran = [&](int row0) {  // B image rows row0..row0+7 (tile-local column index)
@@ -131,6 +146,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
       else grow = n0 + r;
       voff[s] = 2u * (uint32_t)((int64_t)grow * p.ldb + lc * 8);
       ldso[s] = (uint32_t)(G::A_BYTES + row0 * 128);
+      if ((nkt - 1) * BK + lc * 8 >= p.K) tmask |= 1u << s;
       ++s;
     };
 #pragma unroll
@@ -157,23 +173,29 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   auto glds = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t vo, uint32_t so, uint32_t lds_off) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(smem + lds_off), 16, vo, so, 0, 0);
   };
-  // issue slice `part` (1: A0+B0, 2: B1, 3: A1; 0: all) of k-tile kt into stage st
-  auto issue = [&](int part, int kt, int st) {
+  // issue slice `part` (1: A0+B0, 2: B1, 3: A1; 0: all) of k-tile kt into stage st; `masked`: the
+  // partial last k-tile (granules of tmask read out of range = zeros)
+  auto issue_v = [&](int part, int kt, int st, bool masked) {
     const uint32_t so = (uint32_t)kt * (BK * 2), base = (uint32_t)(st * STAGE);
+    auto vo = [&](int i) -> uint32_t { return masked && ((tmask >> i) & 1u) ? kOOB : voff[i]; };
     if (part == 0 || part == 1) {
 #pragma unroll
-      for (int i = 0; i < G::G_A0; ++i) glds(ra, voff[i], so, base + ldso[i]);
+      for (int i = 0; i < G::G_A0; ++i) glds(ra, vo(i), so, base + ldso[i]);
 #pragma unroll
-      for (int i = G::G_A0; i < G::G_P1; ++i) glds(rb, voff[i], so, base + ldso[i]);
+      for (int i = G::G_A0; i < G::G_P1; ++i) glds(rb, vo(i), so, base + ldso[i]);
     }
     if (part == 0 || part == 2) {
 #pragma unroll
-      for (int i = G::G_P1; i < G::G_P1 + G::G_P2; ++i) glds(rb, voff[i], so, base + ldso[i]);
+      for (int i = G::G_P1; i < G::G_P1 + G::G_P2; ++i) glds(rb, vo(i), so, base + ldso[i]);
     }
     if (part == 0 || part == 3) {
 #pragma unroll
-      for (int i = G::G_P1 + G::G_P2; i < G::G_ALL; ++i) glds(ra, voff[i], so, base + ldso[i]);
+      for (int i = G::G_P1 + G::G_P2; i < G::G_ALL; ++i) glds(ra, vo(i), so, base + ldso[i]);
     }
+  };
+  auto issue = [&](int part, int kt, int st) {
+    if (ktail && kt == nkt - 1) issue_v(part, kt, st, true);
+    else issue_v(part, kt, st, false);
   };
 
   // ---- fragment reads: lane row (l&15), 16-B chunk 4·ks + (l>>4) XOR ((l&15)>>1) -----------
@@ -208,7 +230,6 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  const int nkt = p.K / BK;
   // ---- prologue: k-tiles 0 and 1 -------------------------------------------------------------
   issue(0, 0, 0);
   if (nkt > 1) {
@@ -400,7 +421,8 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
         const uint4 v = *reinterpret_cast<const uint4*>(scr + (rr * WTN + cc * 8) * 2);
         const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
         if constexpr (EPI == 0) {
-          *reinterpret_cast<uint4*>(p.c + row * p.ldc + n0 + bcol + cc * 8) = v;
+          const int col = n0 + bcol + cc * 8;
+          if (n0 + BN <= p.N || col < p.N) *reinterpret_cast<uint4*>(p.c + row * p.ldc + col) = v;
         } else if constexpr (EPI == 3) {
           const int col = n0 + bcol + cc * 8;
           uint4 o = v;
@@ -465,7 +487,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
 template <int FN, int EPI>
 void launch_t(const Args& p, hipStream_t s) {
   constexpr int BN = 64 * FN;
-  const int tiles_n = p.N / BN;
+  const int tiles_n = EPI == 0 ? (p.N + BN - 1) / BN : p.N / BN;
   const dim3 grid((unsigned)((p.M / BM) * tiles_n)), block(NT);
   hipLaunchKernelGGL((gemm8_kernel<FN, EPI>), grid, block, 0, s, p);
 }
@@ -481,14 +503,23 @@ int pick_fn(int N, int epi, int half) {
   }
   if (N % 320 == 0) return 5;
   if (N % 256 == 0) return 4;
+  if (epi == 0 && N % 8 == 0 && N > 0) {  // N tail: the width that pads fewer columns (ties: 320)
+    const int p5 = (N + 319) / 320 * 320, p4 = (N + 255) / 256 * 256;
+    return p4 < p5 ? 4 : 5;
+  }
   return 0;
 }
 
 bool launch(const Args& p, int epi, int fn, hipStream_t s) {
-  if (p.M % BM || p.K % BK || p.K < BK) return false;
+  if (p.M % BM || p.M <= 0 || p.N <= 0 || p.K <= 0) return false;
+  // K tail (K % 8 == 0) and N tail (N % 8 == 0): plain C = A·Bᵀ only
+  if (epi == 0 ? (p.K % 8 || p.N % 8) : (p.K % BK != 0)) return false;
   if (fn == 0) fn = pick_fn(p.N, epi, p.half);
   if (fn != 4 && fn != 5) return false;
-  if (p.N % (64 * fn)) return false;
+  if (epi != 0 && p.N % (64 * fn)) return false;
+  // one DMA descriptor per operand with 32-bit offsets: both extents below 2 GiB
+  const int64_t lim = (int64_t)0x7fffffff - (1 << 20);
+  if (((int64_t)(BM - 1) * p.lda + p.K) * 2 >= lim || ((int64_t)(p.N - 1) * p.ldb + p.K) * 2 >= lim) return false;
 #define CS336_G8(F, E)        \
   do {                        \
     launch_t<F, E>(p, s);     \

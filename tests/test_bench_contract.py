@@ -65,6 +65,21 @@ def test_bench_multirank_json(nproc, extra):
         assert r["ms"] > 0 and r["algbw_gbs"] > 0
         assert r["busbw_gbs"] == pytest.approx(r["algbw_gbs"] * 2 * (nproc - 1) / nproc, rel=0.01)
     assert dd["coresidency_caps"] == {"TENSILE_STREAMK_MAX_CUS": "248", "NCCL_MAX_NCHANNELS": "32"}
+    # per-rank CPU affinity
+    assert [a["rank"] for a in dd["cpu_affinity"]] == list(range(nproc))
+    assert all("cpus" in a and "pinned" in a for a in dd["cpu_affinity"])
+    # the handout's DDP-variant table + ZeRO-1 memory; not run under ZeRO-2
+    if "zero" not in extra:
+        rows = dd["ddp_variants"]
+        assert [(r["variant"], r["bucket_mb"]) for r in rows] == [
+            ("naive", None), ("flat", None), ("individual", None), ("bucketed", 1.0), ("bucketed", 10.0),
+            ("bucketed", 100.0), ("bucketed", 1000.0)]
+        for r in rows:
+            assert "error" not in r, r
+            assert r["ms_per_step"] > 0 and 0 <= r["comm_wait_ms"] <= r["ms_per_step"]
+        zm = dd["zero1_memory"]
+        assert set(zm["zero1"]) == {"after_init_mib", "peak_before_step_mib", "peak_after_step_mib"}
+        assert dd["ddp_sweep"]["world"] == nproc and dd["ddp_sweep"]["wall_s"] < 120
     if "--grad-comm-dtype" in extra:
         assert d["config"]["grad_comm_dtype"] == "bf16" and dd["wire_dtype"] == "bfloat16"
         assert dd["wire_mb_total"] == pytest.approx(dd["bucket_mb"]["total"] / 2, rel=0.01)
@@ -88,3 +103,18 @@ def test_bench_world_size_mismatch_fails():
     out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--model", "tiny", "--steps", "1"], cwd=REPO, env=env,
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 2 and "WORLD_SIZE" in out.stderr
+
+
+def test_train_applies_coresidency_env():
+    """train.py sets the multi-rank co-residency env before torch loads, as bench.py does."""
+    from cs336_systems.rccl_env import multi_gpu_env
+
+    code = ("import os, sys, cs336_systems.train as t; "
+            "print(sorted((k, os.environ.get(k)) for k in t._CORES_ENV), 'torch' in sys.modules)")
+    env = {k: v for k, v in os.environ.items() if k not in ("TENSILE_STREAMK_MAX_CUS", "NCCL_MAX_NCHANNELS")}
+    for ws, want in (("2", multi_gpu_env(2)), ("1", {})):
+        env["WORLD_SIZE"] = ws
+        out = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True,
+                             timeout=120)
+        assert out.returncode == 0, out.stderr[-2000:]
+        assert out.stdout.split(" True")[0].strip() == str(sorted(want.items()))

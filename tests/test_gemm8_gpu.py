@@ -93,3 +93,38 @@ def test_gemm8_xl_shapes():
         cs.gemm8(a, b, c, 0, 0, None, None, 0)
         ref = torch.mm(a, b.t())  # hipBLASLt bf16 (fp32 accumulate)
         assert _rel(c, ref) < 5e-3, (N, K)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 10000, 1600), (512, 1600, 10000), (256, 328, 72), (256, 88, 200),
+                                   (768, 10000, 10000)])
+def test_gemm8_tails(M, N, K):
+    """N and K tails (multiples of 8; the vocabulary head's forward N = 10000 and input gradient
+    K = 10000): out-of-range B rows and K chunks load as zeros, partial-tile stores are masked."""
+    cs = _cs()
+    a, b = _rand(M, K, seed=11), _rand(N, K, scale=0.1, seed=12)
+    # NaN guards just past both operands (a K-tail chunk or B row read as data would poison C)
+    abuf = torch.full((M + 1, K), float("nan"), device="cuda", dtype=torch.bfloat16)
+    bbuf = torch.full((N + 1, K), float("nan"), device="cuda", dtype=torch.bfloat16)
+    abuf[:M].copy_(a)
+    bbuf[:N].copy_(b)
+    cbuf = torch.zeros(M, N + 8, device="cuda", dtype=torch.bfloat16)
+    c = cbuf[:, :N]
+    cs.gemm8(abuf[:M], bbuf[:N], c, 0, 0, None, None, 0)
+    ref = a.float() @ b.float().t()
+    assert torch.isfinite(c.float()).all()
+    assert _rel(c, ref) < 5e-3
+    assert torch.count_nonzero(cbuf[:, N:]) == 0  # nothing stored past N
+
+
+def test_gemm8_tail_strided():
+    """K tail with a row stride wider than K (a padded buffer): the tail chunks read zeros, not the
+    padding."""
+    cs = _cs()
+    M, N, K = 256, 1600, 10000
+    abuf = torch.full((M, K + 48), 7.0, device="cuda", dtype=torch.bfloat16)
+    a = abuf[:, :K]
+    a.copy_(_rand(M, K, seed=13))
+    b = _rand(N, K, scale=0.1, seed=14)
+    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    cs.gemm8(a, b, c, 0, 0, None, None, 0)
+    assert _rel(c, a.float() @ b.float().t()) < 5e-3

@@ -75,3 +75,26 @@ def test_gemm8w_xl_w13():
     cs.gemm8w(dy, x, out, 1, False, False, 0)
     ref = torch.mm(dy.t(), x, out_dtype=torch.float32)
     assert _rel(out, ref) < 1e-4
+
+
+def test_gemm8w_past_2gib_chunked():
+    """A dY whose extent passes the kernel's 2 GiB DMA range (row stride of a 50304-column buffer,
+    49152 tokens = 4.9 GB): the binding cuts the token range into chunks that accumulate; split-K
+    plans that would overflow fall back to one split."""
+    from cs336_systems.ops import gemm
+
+    cs = _cs()
+    T, V, d = 49152, 50304, 256
+    buf = torch.empty(T, V, device="cuda", dtype=torch.bfloat16)
+    dy = buf[:, :512]
+    dy.copy_(_rand(T, 512, seed=7))
+    x = _rand(T, d, seed=8)
+    out = torch.full((512, d), float("nan"), device="cuda")
+    cs.gemm8w(dy, x, out, 1, False, False, 0)
+    ref = torch.mm(dy.t(), x, out_dtype=torch.float32)
+    assert _rel(out, ref) < 1e-4
+    with pytest.raises(RuntimeError, match="2 GiB"):
+        cs.gemm8w(dy, x, torch.empty(4, 512, d, device="cuda"), 4, False, False, 0)
+    got = gemm.mm_dw(dy, x)  # plan + fallback through the Python path
+    assert _rel(got, ref) < 1e-4
+    del buf

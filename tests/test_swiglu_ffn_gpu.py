@@ -58,3 +58,34 @@ def test_fused_ffn_matches_unfused_and_fp32(monkeypatch, d_model, d_ff):
                               (gf[2], gu[2], w2r.grad, "dw2")):
         assert _rel(got, r) < 2e-2, (name, _rel(got, r), _rel(unf, r))
         assert _rel(got, unf) < 2e-2, (name, _rel(got, unf))
+
+
+def test_fused_ffn_retain_graph_and_version_check(monkeypatch):
+    """The stages' saved tensors go through the Function's save_for_backward: a
+    retain_graph second backward gives the same gradients, and a saved weight rewritten in place
+    before backward is caught by autograd's version counter instead of used silently."""
+    from cs336_systems.models.fused import attach_bf16_shadows, get_shadow_t
+
+    m, x, dy = _setup(320, 640)
+    attach_bf16_shadows(m)
+    monkeypatch.setenv("CS336_SWIGLU_FUSED", "1")
+    xx = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = m(xx)
+    out.backward(dy, retain_graph=True)
+    g1 = [p.grad.clone() for p in (m.w1.weight, m.w3.weight, m.w2.weight)] + [xx.grad.clone()]
+    for p in m.parameters():
+        p.grad = None
+    xx.grad = None
+    out.backward(dy)
+    g2 = [p.grad for p in (m.w1.weight, m.w3.weight, m.w2.weight)] + [xx.grad]
+    for a, b in zip(g1, g2):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    # a saved Wᵀ shadow bumped in place between forward and backward
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = m(x.clone().requires_grad_(True))
+    wt = get_shadow_t(m.w2.weight)
+    assert wt is not None
+    wt.add_(0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        out.backward(dy)
