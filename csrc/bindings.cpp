@@ -141,6 +141,19 @@ std::tuple<at::Tensor, at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor&
   cs336::AttnParams p;
   fill_attn(p, q, k, v, o, lse, causal, scale);
   set_rope(p, q, k, rope_cos, rope_sin, rope_pos);
+  // split-KV when the query blocks cannot fill the chip (CS336_FA_SPLITS=n forces n, 1 = off)
+  const int force_splits = [] {  // read per call (cheap next to a launch): tests switch it in-process
+    const char* e = std::getenv("CS336_FA_SPLITS");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  const int splits = force_splits > 0 ? force_splits : cs336::flash_attn_fwd_splits(p);
+  at::Tensor ws;
+  if (splits > 1) {
+    ws = at::empty({(int64_t)cs336::flash_attn_fwd_split_workspace(p, splits)}, q.options().dtype(at::kFloat));
+    p.kv_splits = splits;
+    p.opart = ws.data_ptr<float>();
+    p.lpart = p.opart + (int64_t)splits * p.B * p.H * p.Nq * p.D;
+  }
   cs336::flash_attn_fwd(p, to_dtype(q), stream());
   return {o, lse};
 }
@@ -233,16 +246,19 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
   bp.dq_sb = dq.stride(0); bp.dq_sh = dq.stride(1); bp.dq_sn = dq.stride(2);
   bp.dk_sb = dk.stride(0); bp.dk_sh = dk.stride(1); bp.dk_sn = dk.stride(2);
   bp.dv_sb = dv.stride(0); bp.dv_sh = dv.stride(1); bp.dv_sn = dv.stride(2);
-  // CS336_FA_BWD: unset = the fused one-kernel backward (fa_bwd_fused.hip) where it applies and the
-  // (batch, head) workgroups fill the chip (B·H >= 512); 1 = fused wherever it applies; 0 = the
-  // two-kernel form (dQ kernel + dK/dV kernel)
+  // CS336_FA_BWD selects the backward:
+  //   unset: the head-sequential fused kernel (fa_bwd_fused.hip) where it applies and the (batch,
+  //          head) workgroups fill the chip (B·H >= 512), else the key-block-parallel fused kernel
+  //          (fa_bwd_kp.hip, dQ by fp32 atomics) where it applies, else the two-kernel form;
+  //   1: head-sequential wherever it applies (then as unset); 2: key-block parallel wherever it
+  //   applies; 0: the two-kernel form (dQ kernel + dK/dV kernel: deterministic, any shape).
   const int mode = [] {
     const char* e = std::getenv("CS336_FA_BWD");
     return e && *e ? std::atoi(e) : -1;
   }();
   const int64_t nbh = q.size(0) * q.size(1);
   at::Tensor dq_acc;
-  if (mode != 0 && (mode == 1 || nbh >= 512)) {
+  if (mode != 0 && mode != 2 && (mode == 1 || nbh >= 512)) {
     // partial sums exist only for rows with more than one 256-key block
     dq_acc = at::empty({q.size(2) > 256 ? nbh * q.size(2) * 64 : 4}, q.options().dtype(at::kFloat));
     bp.dq_acc = dq_acc.data_ptr<float>();
@@ -274,6 +290,11 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
       return;
     }
     bp.dq_acc = nullptr;
+  }
+  if (mode != 0 && cs336::flash_attn_bwd_kp_ok(bp, to_dtype(q))) {
+    at::Tensor ws = at::empty({(int64_t)cs336::flash_attn_bwd_kp_workspace(bp)}, q.options().dtype(at::kFloat));
+    cs336::flash_attn_bwd_kp(bp, to_dtype(q), ws.data_ptr<float>(), stream());
+    return;
   }
   at::Tensor delta = at::empty({2, q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
   bp.delta = delta.data_ptr<float>();

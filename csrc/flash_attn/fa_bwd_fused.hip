@@ -399,8 +399,15 @@ void launch_fused_c(const AttnBwdParams& bp, hipStream_t s) {
 
 bool flash_attn_bwd_fused_ok(const AttnBwdParams& bp, DType t) {
   const AttnParams& p = bp.f;
-  return t != DType::F32 && p.D == 64 && p.Nq == p.Nk && p.Nq % 64 == 0 && p.Nq > 0 && p.Nq <= fa::FMAXN &&
-         p.rope_cos == nullptr && bp.dq_acc != nullptr;
+  if (!(t != DType::F32 && p.D == 64 && p.Nq == p.Nk && p.Nq % 64 == 0 && p.Nq > 0 && p.Nq <= fa::FMAXN &&
+        p.rope_cos == nullptr && bp.dq_acc != nullptr))
+    return false;
+  // the kernel keeps row strides in 32-bit registers and addresses a head's rows with 32-bit DMA
+  // offsets (s·64·stride·2 B): every row stride must fit int32 and N rows of it stay below 2 GiB
+  // (lse (B, H, N) contiguity is checked by the binding)
+  for (int64_t st : {p.q_sn, p.k_sn, p.v_sn, p.o_sn, bp.do_sn, bp.dq_sn, bp.dk_sn, bp.dv_sn})
+    if (st <= 0 || st > INT32_MAX || (int64_t)p.Nq * st * 2 >= ((int64_t)1 << 31)) return false;
+  return true;
 }
 
 void flash_attn_bwd_fused(const AttnBwdParams& bp, DType t, hipStream_t s) {

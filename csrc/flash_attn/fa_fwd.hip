@@ -16,6 +16,8 @@
 // LSE (natural log, fp32, (B,H,Nq)) is the single extra tensor the backward needs.
 #include "fa_common.h"
 
+#include <algorithm>
+
 namespace cs336 {
 namespace fa {
 
@@ -64,8 +66,10 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
   const int l32 = lane & 31, hh = lane >> 5;
 
   const int nqb = (p.Nq + BM - 1) / BM;
+  // split-KV (p.kv_splits > 1, low parallelism): consecutive blocks are the key splits of one query block
+  const int nsplit = p.kv_splits, sp = (int)(blockIdx.x % (unsigned)nsplit);
   int bh, qb;
-  tile_order(blockIdx.x, p.B * p.H, nqb, CAUSAL ? p.order : 0, p.lpt_group, bh, qb);
+  tile_order((int)(blockIdx.x / (unsigned)nsplit), p.B * p.H, nqb, CAUSAL ? p.order : 0, p.lpt_group, bh, qb);
   if (CAUSAL) qb = nqb - 1 - qb;
   const int b = bh / p.H, h = bh % p.H;
   const int q0 = qb * BM;
@@ -94,7 +98,11 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
   }
 
   const int kv_end = CAUSAL ? min(p.Nk, q0 + BM) : p.Nk;
-  const int ntiles = (kv_end + BN - 1) / BN;
+  // this block's key tiles: [jt0, jt0 + ntiles) of the query block's range (all of it unless split);
+  // tile indices j below are relative to jt0
+  const int ntiles_all = (kv_end + BN - 1) / BN;
+  const int jt0 = (int)((int64_t)ntiles_all * sp / nsplit);
+  const int ntiles = (int)((int64_t)ntiles_all * (sp + 1) / nsplit) - jt0;
 
   uint4 kst[LPT], vst[LPT];
   RopeCoef kst_rc[ROPE ? LPT : 1];  // rotation applied at LDS-write time (keeps the prefetch async)
@@ -103,7 +111,7 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i;
       const int r = c / CPR, ch = c % CPR;
-      const int key = j * BN + r;
+      const int key = (jt0 + j) * BN + r;
       if (ROPE) kst_rc[i] = rope_coef<T>(rope, key < p.Nk ? (rpos ? rpos[key] : key) : 0, ch < CREAL ? ch * EPC : 0);
       if (key < p.Nk && (CREAL == CPR || ch < CREAL)) {
         kst[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)key * p.k_sn + ch * EPC);
@@ -136,7 +144,7 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
   // between this tile's softmax VALU work: s_tile = S^T = K Q^T (Ks: the tile's K image);
   // finish = mask, online softmax, O^T += V^T P^T (Vs: the tile's V image), with `mid` issued after
   // the rescale branch, in the same basic block as the exp2 loop and the PV MFMAs
-  auto active = [&](int j) { return !CAUSAL || j * BN <= qw0 + 31; };
+  auto active = [&](int j) { return !CAUSAL || (jt0 + j) * BN <= qw0 + 31; };
   auto s_tile = [&](const char* Ks, f32x16 (&s)[2]) {
     // ---- S^T = K Q^T ----
 #pragma unroll
@@ -160,7 +168,7 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
     }
   };
   auto finish = [&](int j, const char* Vs, f32x16 (&s)[2], auto&& mid) {
-    const int kt0 = j * BN;
+    const int kt0 = (jt0 + j) * BN;
     // ---- mask (bounds / causal diagonal) ----
     const bool need_mask = (kt0 + BN > p.Nk) || (CAUSAL && kt0 + BN - 1 > qw0);
     if (need_mask) {
@@ -252,12 +260,12 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
       __syncthreads();
     }
     auto issue_k = [&](int j) {
-      const int rows = min(BN, p.Nk - j * BN);
-      kd.issue(Kp + (int64_t)j * BN * p.k_sn, rows, p.k_sn, Kr + (j % NS) * TILE, wave);
+      const int rows = min(BN, p.Nk - (jt0 + j) * BN);
+      kd.issue(Kp + (int64_t)(jt0 + j) * BN * p.k_sn, rows, p.k_sn, Kr + (j % NS) * TILE, wave);
     };
     auto issue_v = [&](int j) {
-      const int rows = min(BN, p.Nk - j * BN);
-      vd.issue(Vp + (int64_t)j * BN * p.v_sn, rows, p.v_sn, Vr + (j % NS) * TILE, wave);
+      const int rows = min(BN, p.Nk - (jt0 + j) * BN);
+      vd.issue(Vp + (int64_t)(jt0 + j) * BN * p.v_sn, rows, p.v_sn, Vr + (j % NS) * TILE, wave);
     };
     // prologue: K(0), V(0), K(1), V(1), ..., K(NS-2), V(NS-2), K(NS-1)
 #pragma unroll
@@ -306,9 +314,9 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
     }
     auto issue = [&](int j) {
       char* Ks = smem + (j % NS) * 2 * TILE;
-      const int rows = min(BN, p.Nk - j * BN);
-      kd.issue(Kp + (int64_t)j * BN * p.k_sn, rows, p.k_sn, Ks, wave);
-      vd.issue(Vp + (int64_t)j * BN * p.v_sn, rows, p.v_sn, Ks + TILE, wave);
+      const int rows = min(BN, p.Nk - (jt0 + j) * BN);
+      kd.issue(Kp + (int64_t)(jt0 + j) * BN * p.k_sn, rows, p.k_sn, Ks, wave);
+      vd.issue(Vp + (int64_t)(jt0 + j) * BN * p.v_sn, rows, p.v_sn, Ks + TILE, wave);
     };
 #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
@@ -367,8 +375,28 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
   }
 
   // ---- epilogue ----
+  // (an empty key split of the DMA-2 ring issued its prologue and never reached the draining `last`)
+  if constexpr (DMA == 2) wait_vmcnt<0>();
   l += __shfl_xor(l, 32, 64);
   const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (nsplit > 1) {
+    // split-KV partial: normalized fp32 O of this key range and its natural-log LSE (merge kernel)
+    if (valid_q) {
+      const int64_t prow = ((int64_t)sp * p.B * p.H + bh) * p.Nq + qrow;
+      float* orow = p.opart + prow * D;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = dt * 32 + 8 * g + 4 * hh;
+          if (DP == D || d < D)
+            *reinterpret_cast<float4*>(orow + d) =
+                make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+        }
+      if (hh == 0) p.lpart[prow] = l > 0.f ? (m + __log2f(l)) * kLn2 : -INFINITY;
+    }
+    return;
+  }
   if (valid_q) {
     S* orow = Op + (int64_t)qrow * p.o_sn;
 #pragma unroll
@@ -448,12 +476,49 @@ void launch_fwd_c(const AttnParams& p, hipStream_t s, dim3 grid, dim3 block) {
   }
 }
 
+// merge of the split-KV partials: lse = log Σ exp(lse_s), O = Σ exp(lse_s - lse) · O_s; one thread per
+// 4 consecutive d of a row
+template <typename T, int D>
+__global__ __launch_bounds__(256) void fa_fwd_merge_kernel(const AttnParams p) {
+  typedef typename Elem<T>::storage S;
+  constexpr int Q4 = (D + 3) / 4;
+  const int64_t rows = (int64_t)p.B * p.H * p.Nq;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= rows * Q4) return;
+  const int64_t row = gid / Q4;
+  const int d = 4 * (int)(gid % Q4);
+  const int bh = (int)(row / p.Nq), n = (int)(row % p.Nq);
+  const int b = bh / p.H, h = bh % p.H;
+  float mx = -INFINITY;
+  for (int sp = 0; sp < p.kv_splits; ++sp) mx = fmaxf(mx, p.lpart[sp * rows + row]);
+  float den = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (mx > -INFINITY) {
+    for (int sp = 0; sp < p.kv_splits; ++sp) {
+      const float w = __expf(p.lpart[sp * rows + row] - mx);
+      const float4 v = *reinterpret_cast<const float4*>(p.opart + (sp * rows + row) * D + d);
+      den += w;
+      a0 = fmaf(w, v.x, a0);
+      a1 = fmaf(w, v.y, a1);
+      a2 = fmaf(w, v.z, a2);
+      a3 = fmaf(w, v.w, a3);
+    }
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+  S* orow = (S*)p.o + b * p.o_sb + h * p.o_sh + (int64_t)n * p.o_sn;
+  store4<T>(orow + d, make_float4(a0 * inv, a1 * inv, a2 * inv, a3 * inv));
+  if (d == 0) p.lse[row] = den > 0.f ? mx + __logf(den) : -INFINITY;
+}
+
 template <typename T, int D>
 void launch_fwd(const AttnParams& p, hipStream_t s) {
   const int nqb = (p.Nq + 127) / 128;
-  const dim3 grid((unsigned)(nqb * p.B * p.H)), block(256);
+  const dim3 grid((unsigned)(nqb * p.B * p.H * p.kv_splits)), block(256);
   if (p.causal) launch_fwd_c<T, D, true>(p, s, grid, block);
   else launch_fwd_c<T, D, false>(p, s, grid, block);
+  if (p.kv_splits > 1) {
+    const int64_t quads = (int64_t)p.B * p.H * p.Nq * ((D + 3) / 4);
+    hipLaunchKernelGGL((fa_fwd_merge_kernel<T, D>), dim3((unsigned)((quads + 255) / 256)), block, 0, s, p);
+  }
 }
 
 template <typename T>
@@ -483,6 +548,22 @@ void launch_fwd_d(const AttnParams& p, hipStream_t s) {
 }
 
 }  // namespace fa
+
+// Split the keys when the (query block, head) workgroups cannot fill the chip (the reference sweep's
+// B 1, H 1): enough splits for ~2 workgroups per CU, each split at least 4 key tiles (256 keys).
+int flash_attn_fwd_splits(const AttnParams& p) {
+  if (p.ot != nullptr || p.D % 4 || p.B * p.H == 0) return 1;
+  const int64_t wgs = (int64_t)((p.Nq + 127) / 128) * p.B * p.H;
+  const int tiles = (p.Nk + 63) / 64;
+  if (wgs >= 256 || tiles < 8) return 1;
+  int sp = (int)std::min<int64_t>((512 + wgs - 1) / wgs, tiles / 4);
+  return std::max(1, std::min(sp, 16));
+}
+
+size_t flash_attn_fwd_split_workspace(const AttnParams& p, int splits) {
+  const size_t rows = (size_t)splits * p.B * p.H * p.Nq;
+  return rows * (size_t)p.D + rows;
+}
 
 void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s) {
   if (p.B * p.H == 0 || p.Nq == 0) return;

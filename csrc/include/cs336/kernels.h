@@ -146,6 +146,13 @@ struct AttnParams {
   // also goes to ot[(h * D + d) * ot_ld + b * Nq + n] (token-contiguous rows, ot_ld = B * Nq)
   void* ot = nullptr;
   int64_t ot_ld = 0;
+  // forward split over the keys (low parallelism: few heads x few query blocks): kv_splits > 1
+  // workgroups per query block, each over one contiguous range of key tiles, write a normalized fp32
+  // partial O (opart [split][B·H][Nq][D]) and its natural-log LSE (lpart [split][B·H][Nq]); a merge
+  // kernel combines them into o and lse (flash_attn_fwd)
+  int kv_splits = 1;
+  float* opart = nullptr;
+  float* lpart = nullptr;
 };
 
 struct AttnBwdParams {
@@ -167,9 +174,17 @@ struct AttnBwdParams {
 };
 
 void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s);
+// key splits the forward uses for p (1 = none) and the fp32 workspace they need (floats)
+int flash_attn_fwd_splits(const AttnParams& p);
+size_t flash_attn_fwd_split_workspace(const AttnParams& p, int splits);
 void flash_attn_bwd(const AttnBwdParams& p, DType t, hipStream_t s);
 // one-kernel backward, one workgroup per (batch, head): 16-bit, d 64, Nq == Nk, N % 64 == 0, N <= 1024
 bool flash_attn_bwd_fused_ok(const AttnBwdParams& p, DType t);
 void flash_attn_bwd_fused(const AttnBwdParams& p, DType t, hipStream_t s);
+// one-kernel backward, one workgroup per 256-key block, dQ by fp32 atomics (fa_bwd_kp.hip): 16-bit,
+// d 64 / 80, Nq == Nk, N % 64 == 0; ws = flash_attn_bwd_kp_workspace(p) floats
+bool flash_attn_bwd_kp_ok(const AttnBwdParams& p, DType t);
+size_t flash_attn_bwd_kp_workspace(const AttnBwdParams& p);
+void flash_attn_bwd_kp(const AttnBwdParams& p, DType t, float* ws, hipStream_t s);
 
 }  // namespace cs336

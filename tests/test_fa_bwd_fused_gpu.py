@@ -93,3 +93,73 @@ def test_fused_rope_out_only_in_step_layout(monkeypatch):
     two = run()
     assert torch.equal(default, fused)
     torch.testing.assert_close(fused.float(), two.float(), rtol=2e-2, atol=2e-2)
+
+
+# ---- key-block-parallel fused backward (csrc/flash_attn/fa_bwd_kp.hip, dQ by fp32 atomics) ----
+def _inputs_d(B, H, N, D, dt, seed=0):
+    torch.manual_seed(seed)
+    mk = lambda: torch.randn(B, N, H, D, device=DEV, dtype=dt).transpose(1, 2)  # noqa: E731
+    return mk(), mk(), mk(), mk()
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("N,D", [(64, 64), (256, 64), (320, 64), (512, 64), (1024, 64), (2048, 64),
+                                 (64, 80), (320, 80), (1024, 80)])
+def test_kp_bwd_vs_fp64(dt, causal, N, D, monkeypatch):
+    monkeypatch.setenv("CS336_FA_BWD", "2")
+    B, H = 2, 3
+    q, k, v, do = _inputs_d(B, H, N, D, dt)
+    hip = _hip()
+    sc = D**-0.5
+    o, lse = hip.fa_fwd(q, k, v, causal, sc)
+    dq, dk, dv = hip.fa_bwd(do, q, k, v, o, lse, causal, sc)
+    rq, rk, rv = _ref(q, k, v, do, causal)
+    for a, b, name in ((dq, rq, "dq"), (dk, rk, "dk"), (dv, rv, "dv")):
+        assert torch.isfinite(a).all(), name
+        err = (a.double() - b).abs().max().item()
+        scale = b.abs().max().item()
+        assert err <= 2e-2 * max(1.0, scale), f"{name}: max err {err} (ref max {scale})"
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("D", [64, 80])
+def test_kp_matches_two_kernel_long(causal, D, monkeypatch):
+    """The reference FA benchmark's regime: few heads, long N (B·H 8, N 4096)."""
+    B, H, N = 2, 4, 4096
+    q, k, v, do = _inputs_d(B, H, N, D, torch.bfloat16, seed=3)
+    hip = _hip()
+    o, lse = hip.fa_fwd(q, k, v, causal, D**-0.5)
+    monkeypatch.setenv("CS336_FA_BWD", "0")
+    two = hip.fa_bwd(do, q, k, v, o, lse, causal, D**-0.5)
+    monkeypatch.delenv("CS336_FA_BWD", raising=False)  # default: B·H < 512 -> key-block parallel
+    kp = hip.fa_bwd(do, q, k, v, o, lse, causal, D**-0.5)
+    for a, b in zip(kp, two):
+        torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("D", [64, 80])
+def test_kp_rope_out_only_in_step_layout(D, monkeypatch):
+    """The 2.7b step's call shape: strided views of one fused d(qkv) buffer, q/k already rotated,
+    dq/dk returned w.r.t. the un-rotated inputs (dK rotated back in its store, dQ in the convert)."""
+    B, H, N = 3, 4, 1024
+    torch.manual_seed(4)
+    qkv = torch.randn(B, N, 3, H, D, device=DEV, dtype=torch.bfloat16)
+    q, k, v = qkv[:, :, 0].transpose(1, 2), qkv[:, :, 1].transpose(1, 2), qkv[:, :, 2].transpose(1, 2)
+    do = torch.randn(B, N, H, D, device=DEV, dtype=torch.bfloat16).transpose(1, 2)
+    re = RotaryEmbedding(2048, D, 10000.0).to(DEV)
+    cos, sin = re.cos.contiguous(), re.sin.contiguous()
+    hip = _hip()
+    o, lse = hip.fa_fwd(q, k, v, True, D**-0.5)
+
+    def run():
+        d = torch.empty(B, N, 3, H, D, device=DEV, dtype=torch.bfloat16)
+        dq, dk, dv = d[:, :, 0].transpose(1, 2), d[:, :, 1].transpose(1, 2), d[:, :, 2].transpose(1, 2)
+        hip.fa_bwd_into(do, q, k, v, o, lse, True, D**-0.5, dq, dk, dv, cos, sin, None, True)
+        return d
+
+    monkeypatch.setenv("CS336_FA_BWD", "2")
+    kp = run()
+    monkeypatch.setenv("CS336_FA_BWD", "0")
+    two = run()
+    torch.testing.assert_close(kp.float(), two.float(), rtol=2e-2, atol=2e-2)

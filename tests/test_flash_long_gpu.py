@@ -126,3 +126,37 @@ def test_flash_dma_forced_short_ragged(monkeypatch, D, causal):
     monkeypatch.setenv("CS336_FA_DMA", "2")
     _run(1, 2, 200, D, causal, [(0, 0), (0, 1)])
     _run(2, 1, 77, D, causal, [(0, 0), (1, 0)])
+
+
+# ---- split-KV forward (low parallelism: the reference sweep's B 1, H 1) ----
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("N,D", [(2048, 64), (4096, 128), (8192, 32), (1024, 16)])
+def test_split_kv_forward_matches(dt, causal, N, D, monkeypatch):
+    """B 1, H 1 takes the split-KV forward by default (partial O + LSE per key split, merged); it
+    must match the unsplit kernel (CS336_FA_SPLITS=1) and an fp64 reference."""
+    from cs336_systems.ops._ext import ops as hip_ops
+
+    if dt == torch.float32 and D == 16:
+        pytest.skip("d 16 is 16-bit only")
+    torch.manual_seed(5)
+    q, k, v = (torch.randn(1, 1, N, D, device="cuda", dtype=dt) for _ in range(3))
+    hip = hip_ops()
+    sc = D**-0.5
+    monkeypatch.setenv("CS336_FA_SPLITS", "1")
+    o1, l1 = hip.fa_fwd(q, k, v, causal, sc)
+    monkeypatch.delenv("CS336_FA_SPLITS")
+    o2, l2 = hip.fa_fwd(q, k, v, causal, sc)
+    monkeypatch.setenv("CS336_FA_SPLITS", "7")  # uneven tile ranges, empty splits under the mask
+    o3, l3 = hip.fa_fwd(q, k, v, causal, sc)
+    s = (q.double() @ k.double().transpose(-1, -2)) * sc
+    if causal:
+        s = s.masked_fill(~torch.ones(N, N, dtype=torch.bool, device="cuda").tril(), float("-inf"))
+    ref_l = torch.logsumexp(s, -1)
+    ref_o = torch.softmax(s, -1) @ v.double()
+    tol = 2e-2 if dt != torch.float32 else 1e-4
+    for o, lse in ((o1, l1), (o2, l2), (o3, l3)):
+        assert torch.isfinite(o).all()
+        assert (o.double() - ref_o).abs().max().item() < tol
+        assert (lse.double() - ref_l).abs().max().item() < tol
+    torch.testing.assert_close(o2.float(), o1.float(), rtol=tol, atol=tol)
