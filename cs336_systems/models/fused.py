@@ -679,6 +679,7 @@ class QKVRopeLinearFn(torch.autograd.Function):
 
         sub.mm_override = mm
         y = FusedLinearFn.forward(sub, x, None, *weights)
+        sub.mm_override = None  # forward-only; the stage lives on as ctx.sub
         ctx.sub = sub
         _stash_saved(ctx, sub)
         return y
@@ -764,7 +765,10 @@ class SwiGLUFFNFn(torch.autograd.Function):
 
         c13.mm_override = mm13
         y = FusedLinearFn.forward(c13, x, None, w1, w3)
-        h = box["h"].view(*x.shape[:-1], -1)
+        h = box.pop("h").view(*x.shape[:-1], -1)
+        # the override is forward-only: the stage outlives this call (ctx.c13, for backward) and its
+        # closure must not keep h alive past the backward that frees the saved copy (+30 GB on XL)
+        c13.mm_override = None
         c2 = _SubCtx((True, False, w2.requires_grad))
         out = FusedLinearFn.forward(c2, h, None, w2)
         ctx.c13, ctx.c2 = c13, c2

@@ -248,8 +248,9 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
   bp.dv_sb = dv.stride(0); bp.dv_sh = dv.stride(1); bp.dv_sn = dv.stride(2);
   // CS336_FA_BWD selects the backward:
   //   unset: the head-sequential fused kernel (fa_bwd_fused.hip) where it applies and the (batch,
-  //          head) workgroups fill the chip (B·H >= 512), else the key-block-parallel fused kernel
-  //          (fa_bwd_kp.hip, dQ by fp32 atomics) where it applies, else the two-kernel form;
+  //          head) workgroups fill the chip (B·H >= 512), else at d 80 the key-block-parallel fused
+  //          kernel (fa_bwd_kp.hip, dQ by fp32 atomics), else the two-kernel form (split over keys /
+  //          queries at low parallelism);
   //   1: head-sequential wherever it applies (then as unset); 2: key-block parallel wherever it
   //   applies; 0: the two-kernel form (dQ kernel + dK/dV kernel: deterministic, any shape).
   const int mode = [] {
@@ -291,7 +292,10 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
     }
     bp.dq_acc = nullptr;
   }
-  if (mode != 0 && cs336::flash_attn_bwd_kp_ok(bp, to_dtype(q))) {
+  // key-block parallel: forced by mode 2; by default only at d 80 (the 2.7b model), where it beats the
+  // two-kernel form (N 4096 causal 466 vs 446 TF, 2.7b step 269 vs 272 ms). At d 64 its dQ atomics
+  // bound it below the two-kernel form (513 vs 625 TF at N 4096 causal): profiles/r4_fa_kp.md
+  if ((mode == 2 || (mode < 0 && q.size(3) == 80)) && cs336::flash_attn_bwd_kp_ok(bp, to_dtype(q))) {
     at::Tensor ws = at::empty({(int64_t)cs336::flash_attn_bwd_kp_workspace(bp)}, q.options().dtype(at::kFloat));
     cs336::flash_attn_bwd_kp(bp, to_dtype(q), ws.data_ptr<float>(), stream());
     return;
@@ -299,6 +303,27 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
   at::Tensor delta = at::empty({2, q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
   bp.delta = delta.data_ptr<float>();
   bp.lrow = bp.delta + q.size(0) * q.size(1) * q.size(2);
+  // low parallelism: split the dQ kernel over keys and the dK/dV kernel over queries (fp32 partial
+  // slabs + reduce); CS336_FA_BWD_SPLITS=1 turns it off
+  int ks = 1, qs = 1;
+  const char* se = std::getenv("CS336_FA_BWD_SPLITS");
+  if (!(se && *se && std::atoi(se) == 1)) cs336::flash_attn_bwd_splits(bp, ks, qs);
+  at::Tensor parts;
+  if (ks > 1 || qs > 1) {
+    parts = at::empty({(int64_t)cs336::flash_attn_bwd_split_workspace(bp, ks, qs)}, q.options().dtype(at::kFloat));
+    float* w = parts.data_ptr<float>();
+    bp.ksplit = ks;
+    bp.qsplit = qs;
+    if (ks > 1) {
+      bp.dq_part = w;
+      w += (int64_t)ks * q.size(0) * q.size(1) * q.size(2) * q.size(3);
+    }
+    if (qs > 1) {
+      const int64_t n = (int64_t)qs * k.size(0) * k.size(1) * k.size(2) * k.size(3);
+      bp.dk_part = w;
+      bp.dv_part = w + n;
+    }
+  }
   cs336::flash_attn_bwd(bp, to_dtype(q), stream());
 }
 

@@ -19,6 +19,8 @@
 // Causal: kernel 1 stops at the diagonal, kernel 2 starts at it; only diagonal tiles are masked.
 #include "fa_common.h"
 
+#include <algorithm>
+
 namespace cs336 {
 namespace fa {
 
@@ -59,8 +61,10 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int l32 = lane & 31, hh = lane >> 5;
   const int nqb = (p.Nq + BM - 1) / BM;
+  // key splits (low parallelism, bp.ksplit > 1): consecutive blocks are the splits of one query block
+  const int nsplit = bp.ksplit, sp = (int)(blockIdx.x % (unsigned)nsplit);
   int bh, qb;
-  tile_order(blockIdx.x, p.B * p.H, nqb, CAUSAL ? p.order : 0, p.lpt_group, bh, qb);
+  tile_order((int)(blockIdx.x / (unsigned)nsplit), p.B * p.H, nqb, CAUSAL ? p.order : 0, p.lpt_group, bh, qb);
   if (CAUSAL) qb = nqb - 1 - qb;
   const int b = bh / p.H, h = bh % p.H;
   const int q0 = qb * BM;
@@ -103,13 +107,16 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   delta += __shfl_xor(delta, 32, 64);
   const float lse2 = valid_q ? p.lse[row_lin] * kLog2e : INFINITY;
   // row constants of the dK/dV kernel, pre-transformed so they load straight into its accumulators
-  if (valid_q && hh == 0) {
+  if (valid_q && hh == 0 && sp == 0) {
     bp.delta[row_lin] = -delta;
     bp.lrow[row_lin] = -lse2;
   }
 
   const int kv_end = CAUSAL ? min(p.Nk, q0 + BM) : p.Nk;
-  const int ntiles = (kv_end + BN - 1) / BN;
+  // this block's key tiles [jt0, jt0 + ntiles) (all unless split); tile indices j are relative to jt0
+  const int ntiles_all = (kv_end + BN - 1) / BN;
+  const int jt0 = (int)((int64_t)ntiles_all * sp / nsplit);
+  const int ntiles = (int)((int64_t)ntiles_all * (sp + 1) / nsplit) - jt0;
 
   uint4 kst[LPT], vst[LPT];
   RopeCoef kst_rc[ROPE == 1 ? LPT : 1];  // rotation applied at LDS-write time (keeps the prefetch async)
@@ -118,7 +125,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i;
       const int r = c / CPR, ch = c % CPR;
-      const int key = j * BN + r;
+      const int key = (jt0 + j) * BN + r;
       if (ROPE == 1) kst_rc[i] = rope_coef<T>(rope, key < p.Nk ? (rpos ? rpos[key] : key) : 0, ch < CREAL ? ch * EPC : 0);
       if (key < p.Nk && (CREAL == CPR || ch < CREAL)) {
         kst[i] = *reinterpret_cast<const uint4*>(Kp + (int64_t)key * p.k_sn + ch * EPC);
@@ -147,7 +154,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
 
   // one K/V tile: S^T, dP^T, dS^T, dQ^T += K^T dS^T (Ks: the tile's K image, V after it)
   auto tile = [&](int j, const char* Ks) __attribute__((always_inline)) {
-    const int kt0 = j * BN;
+    const int kt0 = (jt0 + j) * BN;
     const bool active = !CAUSAL || kt0 <= qw0 + 31;
     if (active) {
       const char* Vs = Ks + TILE;
@@ -232,9 +239,9 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
     }
     auto issue = [&](int j) {
       char* Ks = smem + (j % NS) * 2 * TILE;
-      const int rows = min(BN, p.Nk - j * BN);
-      kd.issue(Kp + (int64_t)j * BN * p.k_sn, rows, p.k_sn, Ks, wave);
-      vd.issue(Vp + (int64_t)j * BN * p.v_sn, rows, p.v_sn, Ks + TILE, wave);
+      const int rows = min(BN, p.Nk - (jt0 + j) * BN);
+      kd.issue(Kp + (int64_t)(jt0 + j) * BN * p.k_sn, rows, p.k_sn, Ks, wave);
+      vd.issue(Vp + (int64_t)(jt0 + j) * BN * p.v_sn, rows, p.v_sn, Ks + TILE, wave);
     };
 #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
@@ -292,6 +299,20 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
     for (; j < ntiles; ++j) step(j, PREFETCH ? (j & 1) : 0);
   }
 
+  if (nsplit > 1) {  // unscaled fp32 partial of this key range (summed by fa_bwd_reduce_kernel)
+    if (valid_q) {
+      float* prow = bp.dq_part + (((int64_t)sp * p.B * p.H + bh) * p.Nq + qrow) * D;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = dt * 32 + 8 * g + 4 * hh;
+          if (DP != D && d >= D) continue;
+          *reinterpret_cast<float4*>(prow + d) = make_float4(dq[dt][4 * g], dq[dt][4 * g + 1], dq[dt][4 * g + 2], dq[dt][4 * g + 3]);
+        }
+    }
+    return;
+  }
   if (valid_q) {
     S* row = dQp + (int64_t)qrow * bp.dq_sn;
     const float sc = p.scale;
@@ -358,8 +379,10 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int l32 = lane & 31, hh = lane >> 5;
   const int nkb = (p.Nk + BK - 1) / BK;
+  // query splits (low parallelism, bp.qsplit > 1): consecutive blocks are the splits of one key block
+  const int nsplit = bp.qsplit, sp = (int)(blockIdx.x % (unsigned)nsplit);
   int bh, kb;  // ascending kb = heaviest first under the causal mask
-  tile_order(blockIdx.x, p.B * p.H, nkb, CAUSAL ? p.order : 0, p.lpt_group, bh, kb);
+  tile_order((int)(blockIdx.x / (unsigned)nsplit), p.B * p.H, nkb, CAUSAL ? p.order : 0, p.lpt_group, bh, kb);
   const int b = bh / p.H, h = bh % p.H;
   const int k0 = kb * BK;
   const int kw0 = k0 + wave * 32;
@@ -394,8 +417,11 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
     }
   }
 
-  const int qt_begin = CAUSAL ? (k0 / BQ) : 0;
-  const int qt_end = (p.Nq + BQ - 1) / BQ;
+  // this block's query tiles [qt_begin, qt_end): the key block's range, or one split of it
+  const int qt_first = CAUSAL ? (k0 / BQ) : 0;
+  const int qt_last = (p.Nq + BQ - 1) / BQ;
+  const int qt_begin = qt_first + (int)((int64_t)(qt_last - qt_first) * sp / nsplit);
+  const int qt_end = qt_first + (int)((int64_t)(qt_last - qt_first) * (sp + 1) / nsplit);
 
   uint4 qst[LPT], dst[LPT];
   RopeCoef qst_rc[ROPE == 1 ? LPT : 1];  // rotation applied at LDS-write time (keeps the prefetch async)
@@ -564,8 +590,8 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
   // Tiles that need the causal mask for some wave (the diagonal ones, qt0 < k0 + BK - 1) and, with
   // LDS-DMA staging, a ragged last tile (rows past Nq are not -inf-padded there) run a masked
   // instantiation of the tile; the bulk runs without the per-element compare/select.
-  const int mask_end = CAUSAL ? min(qt_end, (k0 + BK - 2) / BQ + 1) : qt_begin;
-  const int ragged = (DMA && p.Nq % BQ != 0) ? 1 : 0;
+  const int mask_end = CAUSAL ? min(qt_end, max(qt_begin, (k0 + BK - 2) / BQ + 1)) : qt_begin;
+  const int ragged = (DMA && p.Nq % BQ != 0 && qt_end == qt_last && qt_end > qt_begin) ? 1 : 0;
   if constexpr (DMA) {
     using Dma = TileDma<BQ, RB, CREAL, ES>;
     Dma qd, dd;
@@ -673,6 +699,23 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
     run(mask_end, qt_end, std::false_type{});
   }
 
+  if (nsplit > 1) {  // unscaled fp32 partials of this query range (summed by fa_bwd_reduce_kernel)
+    if (valid_k) {
+      const int64_t prow = (((int64_t)sp * p.B * p.H + bh) * p.Nk + krow) * D;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = dt * 32 + 8 * g + 4 * hh;
+          if (DP != D && d >= D) continue;
+          *reinterpret_cast<float4*>(bp.dk_part + prow + d) =
+              make_float4(dk[dt][4 * g], dk[dt][4 * g + 1], dk[dt][4 * g + 2], dk[dt][4 * g + 3]);
+          *reinterpret_cast<float4*>(bp.dv_part + prow + d) =
+              make_float4(dv[dt][4 * g], dv[dt][4 * g + 1], dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
+        }
+    }
+    return;
+  }
   if (valid_k) {
     S* krow_dk = dKp + (int64_t)krow * bp.dk_sn;
     S* krow_dv = dVp + (int64_t)krow * bp.dv_sn;
@@ -709,10 +752,54 @@ CS336_FA_BWD_DMA(F16, 80)
 CS336_FA_BWD_DMA(F16, 128)
 #undef CS336_FA_BWD_DMA
 
+// sum of `ns` unscaled fp32 split partials ([split][B·H][N][D]) -> out (B, H, N, D strided) = scale ·
+// sum, rotated back by RoPE when `rope` (dQ/dK w.r.t. the un-rotated q/k); one thread per 4 d
+template <typename T, int D>
+__global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(const float* __restrict__ part, int ns, int B, int H, int N,
+                                                            void* out, int64_t sb, int64_t sh, int64_t sn, float scale,
+                                                            const float* rcos, const float* rsin, const int64_t* rpos) {
+  typedef typename Elem<T>::storage S;
+  constexpr int Q4 = D / 4;
+  const int64_t rows = (int64_t)B * H * N;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= rows * Q4) return;
+  const int64_t row = gid / Q4;
+  const int d = 4 * (int)(gid % Q4);
+  float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+  for (int s = 0; s < ns; ++s) {
+    const float4 a = *reinterpret_cast<const float4*>(part + (s * rows + row) * D + d);
+    v0 += a.x; v1 += a.y; v2 += a.z; v3 += a.w;
+  }
+  v0 *= scale; v1 *= scale; v2 *= scale; v3 *= scale;
+  const int bh = (int)(row / N), n = (int)(row % N), b = bh / H, h = bh % H;
+  if (rcos != nullptr) {
+    const Rope rope{rcos, rsin, D / 2};
+    rope_inv4(v0, v1, v2, v3, rope, rpos ? rpos[(int64_t)b * N + n] : n, d);
+  }
+  store4<T>((S*)out + b * sb + h * sh + (int64_t)n * sn + d, make_float4(v0, v1, v2, v3));
+}
+
 template <typename T, int D, bool C, int R, bool DMA>
 void launch_bwd_v(const AttnBwdParams& bp, hipStream_t s, dim3 gq, dim3 gk, dim3 block) {
   hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, C, R, DMA>), gq, block, 0, s, bp);
   hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, C, R, DMA>), gk, block, 0, s, bp);
+  const AttnParams& p = bp.f;
+  const float* rc = R != 0 ? p.rope_cos : nullptr;
+  if (bp.ksplit > 1) {
+    const int64_t q4 = (int64_t)p.B * p.H * p.Nq * (D / 4);
+    hipLaunchKernelGGL((fa_bwd_reduce_kernel<T, D>), dim3((unsigned)((q4 + 255) / 256)), block, 0, s, bp.dq_part,
+                       bp.ksplit, p.B, p.H, p.Nq, bp.dq, bp.dq_sb, bp.dq_sh, bp.dq_sn, p.scale, rc, p.rope_sin,
+                       p.rope_pos);
+  }
+  if (bp.qsplit > 1) {
+    const int64_t k4 = (int64_t)p.B * p.H * p.Nk * (D / 4);
+    const dim3 g((unsigned)((k4 + 255) / 256));
+    hipLaunchKernelGGL((fa_bwd_reduce_kernel<T, D>), g, block, 0, s, bp.dk_part, bp.qsplit, p.B, p.H, p.Nk, bp.dk,
+                       bp.dk_sb, bp.dk_sh, bp.dk_sn, p.scale, rc, p.rope_sin, p.rope_pos);
+    hipLaunchKernelGGL((fa_bwd_reduce_kernel<T, D>), g, block, 0, s, bp.dv_part, bp.qsplit, p.B, p.H, p.Nk, bp.dv,
+                       bp.dv_sb, bp.dv_sh, bp.dv_sn, 1.f, (const float*)nullptr, (const float*)nullptr,
+                       (const int64_t*)nullptr);
+  }
 }
 
 template <typename T, int D, bool C>
@@ -735,7 +822,7 @@ void launch_bwd(const AttnBwdParams& bp, hipStream_t s) {
   const AttnParams& p = bp.f;
   const int nqb = (p.Nq + 127) / 128;
   const int nkb = (p.Nk + 127) / 128;
-  const dim3 gq((unsigned)(nqb * p.B * p.H)), gk((unsigned)(nkb * p.B * p.H)), block(256);
+  const dim3 gq((unsigned)(nqb * p.B * p.H * bp.ksplit)), gk((unsigned)(nkb * p.B * p.H * bp.qsplit)), block(256);
   if (p.causal) launch_bwd_c<T, D, true>(bp, s, gq, gk, block);
   else launch_bwd_c<T, D, false>(bp, s, gq, gk, block);
 }
@@ -767,6 +854,25 @@ void launch_bwd_d(const AttnBwdParams& bp, hipStream_t s) {
 }
 
 }  // namespace fa
+
+// Low parallelism (the reference sweep's B 1, H 1: N/128 query blocks and key blocks on 256 CUs):
+// split the dQ kernel's keys and the dK/dV kernel's queries until each kernel has ~512 workgroups,
+// each split keeping at least 4 tiles of its loop.
+void flash_attn_bwd_splits(const AttnBwdParams& bp, int& ksplit, int& qsplit) {
+  const AttnParams& p = bp.f;
+  ksplit = qsplit = 1;
+  if (p.B * p.H == 0 || p.D % 4) return;
+  const int64_t bh = (int64_t)p.B * p.H;
+  const int64_t nqb = (p.Nq + 127) / 128, nkb = (p.Nk + 127) / 128;
+  if (nqb * bh < 256) ksplit = (int)std::max<int64_t>(1, std::min<int64_t>({(512 + nqb * bh - 1) / (nqb * bh), (p.Nk / 32) / 4, 16}));
+  if (nkb * bh < 256) qsplit = (int)std::max<int64_t>(1, std::min<int64_t>({(512 + nkb * bh - 1) / (nkb * bh), (p.Nq / 32) / 4, 16}));
+}
+
+size_t flash_attn_bwd_split_workspace(const AttnBwdParams& bp, int ksplit, int qsplit) {
+  const AttnParams& p = bp.f;
+  const size_t bh = (size_t)p.B * p.H;
+  return (ksplit > 1 ? ksplit * bh * p.Nq * p.D : 0) + (qsplit > 1 ? 2 * qsplit * bh * p.Nk * p.D : 0);
+}
 
 void flash_attn_bwd(const AttnBwdParams& bp, DType t, hipStream_t s) {
   if (bp.f.B * bp.f.H == 0 || bp.f.Nq == 0 || bp.f.Nk == 0) return;

@@ -93,8 +93,9 @@ struct Geo {
   static_assert((4 * B0C / 8) % 8 == 0 && (4 * (WTN - B0C) / 8) % 8 == 0, "B granules must split over 8 waves");
 };
 
-template <int FN, int EPI>
+template <int FN, int EPI, bool TAIL>
 __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
+  static_assert(!TAIL || EPI == 0, "tails: plain C = A·Bᵀ only");
   using G = Geo<FN>;
   constexpr int BN = G::BN, WTN = G::WTN, FB0 = G::FB0, B0C = G::B0C, STAGE = G::STAGE;
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   // ---- tile coordinates -------------------------------------------------------------------
   // EPI 1: N = 2·half, BN/2 units of each half per tile. EPI 0 also takes an N tail (N % BN != 0,
   // N % 8 == 0: the vocabulary head, 10000 = 31·320 + 80): B rows >= N read zeros, stores masked
-  const int tiles_n = EPI == 0 ? (p.N + BN - 1) / BN : p.N / BN;
+  const int tiles_n = TAIL ? (p.N + BN - 1) / BN : p.N / BN;
   const int tiles_m = p.M / BM;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int per_group = kGroupM * tiles_n;
@@ -120,8 +121,10 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   // ---- DMA setup: per wave G_ALL granules; slot order P1 (A0 then B0), P2 (B1), P3 (A1) ------
   // The record counts end at each operand's last element (host: both extents < 2 GiB), so B rows
   // past N (EPI 0 N tail) and the lanes of a K tail pointed at kOOB read zeros (raw-buffer range check)
-  const int nkt = (p.K + BK - 1) / BK;
-  const bool ktail = (p.K % BK) != 0;  // last k-tile partial (K % 8 == 0): its chunks >= K are zero
+  // (the tail bookkeeping lives in its own instantiation: in the full-tile kernel one more live
+  // register spilled the FN 5 main loop)
+  const int nkt = TAIL ? (p.K + BK - 1) / BK : p.K / BK;
+  const bool ktail = TAIL && (p.K % BK) != 0;  // last k-tile partial (K % 8 == 0): its chunks >= K are zero
   constexpr uint32_t kOOB = 0x7ffffff0u;
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.a + (int64_t)m0 * p.lda), (short)0, (uint32_t)(((BM - 1) * p.lda + p.K) * 2), 0x00020000);
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
       const int r = row0 + (lane >> 3), lc = (lane & 7) ^ ((r >> 1) & 7);
       voff[s] = 2u * (uint32_t)(r * p.lda + lc * 8);
       ldso[s] = (uint32_t)(row0 * 128);
-      if ((nkt - 1) * BK + lc * 8 >= p.K) tmask |= 1u << s;
+      if (TAIL && (nkt - 1) * BK + lc * 8 >= p.K) tmask |= 1u << s;
       ++s;
     };
     auto b_gran = [&](int row0) {  // B image rows row0..row0+7 (tile-local column index)
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
       else grow = n0 + r;
       voff[s] = 2u * (uint32_t)((int64_t)grow * p.ldb + lc * 8);
       ldso[s] = (uint32_t)(G::A_BYTES + row0 * 128);
-      if ((nkt - 1) * BK + lc * 8 >= p.K) tmask |= 1u << s;
+      if (TAIL && (nkt - 1) * BK + lc * 8 >= p.K) tmask |= 1u << s;
       ++s;
     };
 #pragma unroll
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
     }
   };
   auto issue = [&](int part, int kt, int st) {
-    if (ktail && kt == nkt - 1) issue_v(part, kt, st, true);
+    if (TAIL && ktail && kt == nkt - 1) issue_v(part, kt, st, true);
     else issue_v(part, kt, st, false);
   };
 
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
         const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
         if constexpr (EPI == 0) {
           const int col = n0 + bcol + cc * 8;
-          if (n0 + BN <= p.N || col < p.N) *reinterpret_cast<uint4*>(p.c + row * p.ldc + col) = v;
+          if (!TAIL || n0 + BN <= p.N || col < p.N) *reinterpret_cast<uint4*>(p.c + row * p.ldc + col) = v;
         } else if constexpr (EPI == 3) {
           const int col = n0 + bcol + cc * 8;
           uint4 o = v;
@@ -487,9 +490,16 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
 template <int FN, int EPI>
 void launch_t(const Args& p, hipStream_t s) {
   constexpr int BN = 64 * FN;
-  const int tiles_n = EPI == 0 ? (p.N + BN - 1) / BN : p.N / BN;
+  const bool tail = EPI == 0 && (p.N % BN != 0 || p.K % BK != 0);
+  const int tiles_n = tail ? (p.N + BN - 1) / BN : p.N / BN;
   const dim3 grid((unsigned)((p.M / BM) * tiles_n)), block(NT);
-  hipLaunchKernelGGL((gemm8_kernel<FN, EPI>), grid, block, 0, s, p);
+  if constexpr (EPI == 0 && FN == 4) {  // (launch sends every tail problem to FN 4)
+    if (tail) {
+      hipLaunchKernelGGL((gemm8_kernel<FN, 0, true>), grid, block, 0, s, p);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((gemm8_kernel<FN, EPI, false>), grid, block, 0, s, p);
 }
 
 }  // namespace
@@ -503,10 +513,7 @@ int pick_fn(int N, int epi, int half) {
   }
   if (N % 320 == 0) return 5;
   if (N % 256 == 0) return 4;
-  if (epi == 0 && N % 8 == 0 && N > 0) {  // N tail: the width that pads fewer columns (ties: 320)
-    const int p5 = (N + 319) / 320 * 320, p4 = (N + 255) / 256 * 256;
-    return p4 < p5 ? 4 : 5;
-  }
+  if (epi == 0 && N % 8 == 0 && N > 0) return 4;  // N tail: the tail kernel (FN 5 would spill, see launch)
   return 0;
 }
 
@@ -515,6 +522,9 @@ bool launch(const Args& p, int epi, int fn, hipStream_t s) {
   // K tail (K % 8 == 0) and N tail (N % 8 == 0): plain C = A·Bᵀ only
   if (epi == 0 ? (p.K % 8 || p.N % 8) : (p.K % BK != 0)) return false;
   if (fn == 0) fn = pick_fn(p.N, epi, p.half);
+  // a partial k-tile or column tile runs the tail instantiation, at FN 4: its extra per-granule mask
+  // register spills the FN 5 main loop (20 B scratch per lane)
+  if (epi == 0 && (p.K % BK || p.N % (64 * fn))) fn = 4;
   if (fn != 4 && fn != 5) return false;
   if (epi != 0 && p.N % (64 * fn)) return false;
   // one DMA descriptor per operand with 32-bit offsets: both extents below 2 GiB

@@ -171,6 +171,13 @@ struct AttnBwdParams {
   float* lrow;
   // fp32 (B, H, Nq, 64) dQ partial sums of the fused head-sequential backward (fa_bwd_fused.hip)
   float* dq_acc = nullptr;
+  // two-kernel form at low parallelism (flash_attn_bwd_splits): the dQ kernel split over key ranges
+  // (ksplit) and the dK/dV kernel over query ranges (qsplit); each split writes unscaled fp32
+  // partials ([split][B·H][N][D] slabs) that a reduce kernel sums, scales, rotates back and casts
+  int ksplit = 1, qsplit = 1;
+  float* dq_part = nullptr;
+  float* dk_part = nullptr;
+  float* dv_part = nullptr;
 };
 
 void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s);
@@ -178,6 +185,9 @@ void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s);
 int flash_attn_fwd_splits(const AttnParams& p);
 size_t flash_attn_fwd_split_workspace(const AttnParams& p, int splits);
 void flash_attn_bwd(const AttnBwdParams& p, DType t, hipStream_t s);
+// (ksplit, qsplit) the two-kernel backward uses for p at low parallelism, and their fp32 workspace
+void flash_attn_bwd_splits(const AttnBwdParams& p, int& ksplit, int& qsplit);
+size_t flash_attn_bwd_split_workspace(const AttnBwdParams& p, int ksplit, int qsplit);
 // one-kernel backward, one workgroup per (batch, head): 16-bit, d 64, Nq == Nk, N % 64 == 0, N <= 1024
 bool flash_attn_bwd_fused_ok(const AttnBwdParams& p, DType t);
 void flash_attn_bwd_fused(const AttnBwdParams& p, DType t, hipStream_t s);

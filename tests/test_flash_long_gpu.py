@@ -160,3 +160,36 @@ def test_split_kv_forward_matches(dt, causal, N, D, monkeypatch):
         assert (o.double() - ref_o).abs().max().item() < tol
         assert (lse.double() - ref_l).abs().max().item() < tol
     torch.testing.assert_close(o2.float(), o1.float(), rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("N,D", [(2048, 64), (4096, 128), (4096, 32), (1024, 16), (2048, 80)])
+def test_split_backward_matches(dt, causal, N, D, monkeypatch):
+    """B 1, H 1: the two-kernel backward splits the dQ kernel over keys and the dK/dV kernel over
+    queries (fp32 partials + reduce); it must match the unsplit two-kernel form and fp64."""
+    from cs336_systems.ops._ext import ops as hip_ops
+
+    if dt == torch.float32 and D in (16, 80):
+        pytest.skip("d 16 / 80 are 16-bit only")
+    torch.manual_seed(6)
+    q, k, v, do = (torch.randn(1, 1, N, D, device="cuda", dtype=dt) for _ in range(4))
+    hip = hip_ops()
+    sc = D**-0.5
+    o, lse = hip.fa_fwd(q, k, v, causal, sc)
+    monkeypatch.setenv("CS336_FA_BWD", "0")  # the two-kernel form (the split applies to it)
+    monkeypatch.setenv("CS336_FA_BWD_SPLITS", "1")
+    g1 = hip.fa_bwd(do, q, k, v, o, lse, causal, sc)
+    monkeypatch.delenv("CS336_FA_BWD_SPLITS")
+    g2 = hip.fa_bwd(do, q, k, v, o, lse, causal, sc)
+    qr, kr, vr = (t.detach().double().requires_grad_(True) for t in (q, k, v))
+    s = (qr @ kr.transpose(-1, -2)) * sc
+    if causal:
+        s = s.masked_fill(~torch.ones(N, N, dtype=torch.bool, device="cuda").tril(), float("-inf"))
+    (torch.softmax(s, -1) @ vr).backward(do.double())
+    tol = 2e-2 if dt != torch.float32 else 1e-3
+    for a, b, r, name in zip(g2, g1, (qr.grad, kr.grad, vr.grad), ("dq", "dk", "dv")):
+        assert torch.isfinite(a).all(), name
+        err = (a.double() - r).abs().max().item()
+        assert err <= tol * max(1.0, r.abs().max().item()), (name, err)
+        torch.testing.assert_close(a.float(), b.float(), rtol=tol, atol=tol)

@@ -89,3 +89,41 @@ def test_fused_ffn_retain_graph_and_version_check(monkeypatch):
     wt.add_(0)
     with pytest.raises(RuntimeError, match="modified by an inplace operation"):
         out.backward(dy)
+
+
+def test_fused_ffn_backward_frees_each_layers_h(monkeypatch):
+    """Once a layer's backward ran, nothing of its forward (h, y, X) may stay alive for the rest of the
+    backward: with n layers chained, the memory held when the FIRST layer's input gradient arrives
+    must not grow with n beyond the weight gradients (a forward-only closure on the stage once kept
+    every layer's h: +30 GB on the XL step)."""
+    from cs336_systems.models.fused import attach_bf16_shadows
+    from cs336_systems.models.transformer import SwiGLU
+
+    monkeypatch.setenv("CS336_SWIGLU_FUSED", "1")
+    d_model, d_ff, tokens = 320, 1280, 4096
+
+    def held_at_first_grad(n):
+        torch.manual_seed(0)
+        layers = [SwiGLU(d_model, d_ff, device="cuda") for _ in range(n)]
+        for m in layers:
+            m.group_()
+            attach_bf16_shadows(m)
+        x = torch.randn(1, tokens, d_model, device="cuda", requires_grad=True)
+        seen = {}
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            hcur = x * 1.0
+            def hook(g):
+                seen.setdefault("mem", torch.cuda.memory_allocated())
+
+            hcur.register_hook(hook)
+            for m in layers:
+                hcur = m(hcur)
+        hcur.float().sum().backward()
+        grads = sum(p.grad.numel() * 4 for m in layers for p in m.parameters())
+        return seen["mem"] - base - grads
+
+    h_bytes = tokens * d_ff * 2
+    grow = held_at_first_grad(6) - held_at_first_grad(2)
+    assert grow < h_bytes, f"memory held at the first layer's grad grew by {grow / 2**20:.1f} MiB for 4 more layers"
