@@ -93,9 +93,11 @@ struct Geo {
   static_assert((4 * B0C / 8) % 8 == 0 && (4 * (WTN - B0C) / 8) % 8 == 0, "B granules must split over 8 waves");
 };
 
-template <int FN, int EPI, bool TAIL>
+// TAIL: bit 0 = partial last column tile (N % BN), bit 1 = partial last k-tile (K % 64)
+template <int FN, int EPI, int TAIL>
 __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   static_assert(!TAIL || EPI == 0, "tails: plain C = A·Bᵀ only");
+  constexpr bool NTAIL = TAIL & 1, KTAIL = TAIL & 2;
   using G = Geo<FN>;
   constexpr int BN = G::BN, WTN = G::WTN, FB0 = G::FB0, B0C = G::B0C, STAGE = G::STAGE;
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
@@ -107,7 +109,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   // ---- tile coordinates -------------------------------------------------------------------
   // EPI 1: N = 2·half, BN/2 units of each half per tile. EPI 0 also takes an N tail (N % BN != 0,
   // N % 8 == 0: the vocabulary head, 10000 = 31·320 + 80): B rows >= N read zeros, stores masked
-  const int tiles_n = TAIL ? (p.N + BN - 1) / BN : p.N / BN;
+  const int tiles_n = NTAIL ? (p.N + BN - 1) / BN : p.N / BN;
   const int tiles_m = p.M / BM;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int per_group = kGroupM * tiles_n;
@@ -123,8 +125,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   // past N (EPI 0 N tail) and the lanes of a K tail pointed at kOOB read zeros (raw-buffer range check)
   // (the tail bookkeeping lives in its own instantiation: in the full-tile kernel one more live
   // register spilled the FN 5 main loop)
-  const int nkt = TAIL ? (p.K + BK - 1) / BK : p.K / BK;
-  const bool ktail = TAIL && (p.K % BK) != 0;  // last k-tile partial (K % 8 == 0): its chunks >= K are zero
+  const int nkt = KTAIL ? (p.K + BK - 1) / BK : p.K / BK;  // (KTAIL: the last k-tile is partial)
   constexpr uint32_t kOOB = 0x7ffffff0u;
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.a + (int64_t)m0 * p.lda), (short)0, (uint32_t)(((BM - 1) * p.lda + p.K) * 2), 0x00020000);
@@ -132,14 +133,12 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
       (void*)p.b, (short)0, (uint32_t)(((int64_t)(p.N - 1) * p.ldb + p.K) * 2), 0x00020000);
   uint32_t voff[G::G_ALL];   // per-lane byte offset at k-tile 0
   uint32_t ldso[G::G_ALL];   // wave-uniform LDS byte offset within a stage
-  uint32_t tmask = 0;        // granules whose chunk lies past K in the last k-tile
   {
     int s = 0;
     auto a_gran = [&](int row0) {  // A image rows row0..row0+7
       const int r = row0 + (lane >> 3), lc = (lane & 7) ^ ((r >> 1) & 7);
       voff[s] = 2u * (uint32_t)(r * p.lda + lc * 8);
       ldso[s] = (uint32_t)(row0 * 128);
-      if (TAIL && (nkt - 1) * BK + lc * 8 >= p.K) tmask |= 1u << s;
       ++s;
     };
     auto b_gran = [&](int row0) {  // B image rows row0..row0+7 (tile-local column index)
@@ -149,7 +148,6 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
       else grow = n0 + r;
       voff[s] = 2u * (uint32_t)((int64_t)grow * p.ldb + lc * 8);
       ldso[s] = (uint32_t)(G::A_BYTES + row0 * 128);
-      if (TAIL && (nkt - 1) * BK + lc * 8 >= p.K) tmask |= 1u << s;
       ++s;
     };
 #pragma unroll
@@ -176,11 +174,31 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   auto glds = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t vo, uint32_t so, uint32_t lds_off) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(smem + lds_off), 16, vo, so, 0, 0);
   };
+  // image row0 of granule i (slot order, as laid out above): the K-tail mask re-derives a lane's
+  // source chunk from it and the lane id instead of keeping a mask register live through the loop
+  auto gran_row = [&](int i) -> int {
+    if (i < G::G_A0) {
+      const int g = wave + 8 * i;
+      return g < 8 ? 8 * g : 128 + 8 * (g - 8);
+    } else if (i < G::G_P1) {
+      const int g = wave + 8 * (i - G::G_A0), per = B0C / 8;
+      return (g / per) * WTN + (g % per) * 8;
+    } else if (i < G::G_P1 + G::G_P2) {
+      const int g = wave + 8 * (i - G::G_P1), per = (WTN - B0C) / 8;
+      return (g / per) * WTN + B0C + (g % per) * 8;
+    }
+    const int g = wave + 8 * (i - G::G_P1 - G::G_P2);
+    return g < 8 ? 64 + 8 * g : 192 + 8 * (g - 8);
+  };
   // issue slice `part` (1: A0+B0, 2: B1, 3: A1; 0: all) of k-tile kt into stage st; `masked`: the
-  // partial last k-tile (granules of tmask read out of range = zeros)
+  // partial last k-tile (lanes whose chunk lies at or past K read out of range = zeros)
   auto issue_v = [&](int part, int kt, int st, bool masked) {
     const uint32_t so = (uint32_t)kt * (BK * 2), base = (uint32_t)(st * STAGE);
-    auto vo = [&](int i) -> uint32_t { return masked && ((tmask >> i) & 1u) ? kOOB : voff[i]; };
+    auto vo = [&](int i) -> uint32_t {
+      if (!masked) return voff[i];
+      const int ln = __lane_id(), r = gran_row(i) + (ln >> 3), lc = (ln & 7) ^ ((r >> 1) & 7);
+      return kt * BK + lc * 8 >= p.K ? kOOB : voff[i];
+    };
     if (part == 0 || part == 1) {
 #pragma unroll
       for (int i = 0; i < G::G_A0; ++i) glds(ra, vo(i), so, base + ldso[i]);
@@ -197,7 +215,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
     }
   };
   auto issue = [&](int part, int kt, int st) {
-    if (TAIL && ktail && kt == nkt - 1) issue_v(part, kt, st, true);
+    if (KTAIL && kt == nkt - 1) issue_v(part, kt, st, true);
     else issue_v(part, kt, st, false);
   };
 
@@ -425,7 +443,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
         const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
         if constexpr (EPI == 0) {
           const int col = n0 + bcol + cc * 8;
-          if (!TAIL || n0 + BN <= p.N || col < p.N) *reinterpret_cast<uint4*>(p.c + row * p.ldc + col) = v;
+          if (!NTAIL || n0 + BN <= p.N || col < p.N) *reinterpret_cast<uint4*>(p.c + row * p.ldc + col) = v;
         } else if constexpr (EPI == 3) {
           const int col = n0 + bcol + cc * 8;
           uint4 o = v;
@@ -490,16 +508,24 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
 template <int FN, int EPI>
 void launch_t(const Args& p, hipStream_t s) {
   constexpr int BN = 64 * FN;
-  const bool tail = EPI == 0 && (p.N % BN != 0 || p.K % BK != 0);
-  const int tiles_n = tail ? (p.N + BN - 1) / BN : p.N / BN;
+  const int tail = EPI == 0 ? (p.N % BN != 0 ? 1 : 0) | (p.K % BK != 0 ? 2 : 0) : 0;
+  const int tiles_n = (tail & 1) ? (p.N + BN - 1) / BN : p.N / BN;
   const dim3 grid((unsigned)((p.M / BM) * tiles_n)), block(NT);
-  if constexpr (EPI == 0 && FN == 4) {  // (launch sends every tail problem to FN 4)
-    if (tail) {
-      hipLaunchKernelGGL((gemm8_kernel<FN, 0, true>), grid, block, 0, s, p);
+  if constexpr (EPI == 0) {
+    if (tail == 1) {
+      hipLaunchKernelGGL((gemm8_kernel<FN, 0, 1>), grid, block, 0, s, p);
+      return;
+    }
+    if (tail == 2) {
+      hipLaunchKernelGGL((gemm8_kernel<FN, 0, 2>), grid, block, 0, s, p);
+      return;
+    }
+    if (tail == 3) {
+      hipLaunchKernelGGL((gemm8_kernel<FN, 0, 3>), grid, block, 0, s, p);
       return;
     }
   }
-  hipLaunchKernelGGL((gemm8_kernel<FN, EPI, false>), grid, block, 0, s, p);
+  hipLaunchKernelGGL((gemm8_kernel<FN, EPI, 0>), grid, block, 0, s, p);
 }
 
 }  // namespace
@@ -513,7 +539,10 @@ int pick_fn(int N, int epi, int half) {
   }
   if (N % 320 == 0) return 5;
   if (N % 256 == 0) return 4;
-  if (epi == 0 && N % 8 == 0 && N > 0) return 4;  // N tail: the tail kernel (FN 5 would spill, see launch)
+  if (epi == 0 && N % 8 == 0 && N > 0) {  // N tail: the width that pads fewer columns (ties: 320)
+    const int p5 = (N + 319) / 320 * 320, p4 = (N + 255) / 256 * 256;
+    return p4 < p5 ? 4 : 5;
+  }
   return 0;
 }
 
@@ -522,9 +551,6 @@ bool launch(const Args& p, int epi, int fn, hipStream_t s) {
   // K tail (K % 8 == 0) and N tail (N % 8 == 0): plain C = A·Bᵀ only
   if (epi == 0 ? (p.K % 8 || p.N % 8) : (p.K % BK != 0)) return false;
   if (fn == 0) fn = pick_fn(p.N, epi, p.half);
-  // a partial k-tile or column tile runs the tail instantiation, at FN 4: its extra per-granule mask
-  // register spills the FN 5 main loop (20 B scratch per lane)
-  if (epi == 0 && (p.K % BK || p.N % (64 * fn))) fn = 4;
   if (fn != 4 && fn != 5) return false;
   if (epi != 0 && p.N % (64 * fn)) return false;
   // one DMA descriptor per operand with 32-bit offsets: both extents below 2 GiB
