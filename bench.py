@@ -468,6 +468,11 @@ def main(argv=None):
             torch.cuda.empty_cache()
         from cs336_systems.bench.ddp import sweep_variants
 
+        # the sweep's small per-GPU batch has no committed GEMM-table entries; in a multi-rank job those
+        # would run hipBLASLt's stream-K default beside the RCCL all-reduces (rccl_env.py), so the sweep
+        # uses the cs336 kernels only (gemm8 / gemm8w take every projection shape of it)
+        gemm_mode_saved = os.environ.get("CS336_GEMM")
+        os.environ["CS336_GEMM"] = "hip" if device.type == "cuda" else gemm_mode_saved or "blas"
         try:
             sw = sweep_variants(args.model, args.ctx, args.ddp_sweep_batch, device, amp=amp, vocab=args.vocab)
             out["dist"]["ddp_variants"] = sw.pop("variants")
@@ -475,6 +480,11 @@ def main(argv=None):
             out["dist"]["ddp_sweep"] = sw
         except Exception as e:  # noqa: BLE001 - the sweep never costs the headline line
             out["dist"]["ddp_sweep"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        finally:
+            if gemm_mode_saved is None:
+                os.environ.pop("CS336_GEMM", None)
+            else:
+                os.environ["CS336_GEMM"] = gemm_mode_saved
     if tmode == "tune" and rank == 0:
         import torch.cuda.tunable as tunable
 

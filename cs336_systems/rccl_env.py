@@ -9,12 +9,19 @@ GEMM grid holds every CU, an RCCL kernel can be only partially resident: its mis
 wait for CUs held by GEMM workgroups, which wait for undispatched successors, which wait for CUs held
 by the resident RCCL blocks -- a cycle that crosses ranks through the peers' RCCL kernels.
 
-The cut: cap the stream-K grids (``TENSILE_STREAMK_MAX_CUS``) so that a reserve of CUs never holds a
-stream-K workgroup, and cap RCCL's channels (``NCCL_MAX_NCHANNELS``) so that every channel block of a
-collective fits on the reserve by itself. Then an RCCL kernel always becomes fully resident (it
-needs nothing the GEMM holds), finishes when its peers' do, and the GEMM at worst waits for it.
-``scripts/coresidency_probe.py`` / ``tests/test_coresidency_gpu.py`` measure both sides with an
-RCCL-shaped cohort that needs all of its workgroups resident at once.
+The cut, as of round 4: the XL bench step has no stream-K kernel left. Every projection GEMM of it,
+the vocabulary head included (gemm8 N / K tails), is a cs336 kernel whose workgroups never wait for
+other workgroups (committed GEMM table; `profiles/r4_xl_roofline_b96.md` lists no Tensile kernel),
+and bench.py's multi-rank DDP-variant sweep runs with ``CS336_GEMM=hip`` for the same reason. What
+remains is a cap on stream-K grids (``TENSILE_STREAMK_MAX_CUS``) for any hipBLASLt GEMM that still
+runs in a multi-rank job (a shape outside the table takes hipBLASLt's default untimed): it keeps a
+reserve of CUs free of stream-K workgroups, where RCCL channel blocks (256 threads, 21 KB LDS, <= 128
+VGPRs: several per CU) can always become resident. It costs the bench nothing (no hipBLASLt GEMM runs
+in its step). The RCCL channel cap of round 3 (``NCCL_MAX_NCHANNELS=32``) is dropped: it only bought
+safety beside stream-K grids, which the step no longer has, and it capped the all-reduce bandwidth of
+every collective. ``scripts/coresidency_probe.py`` / ``tests/test_coresidency_gpu.py`` measure the
+stream-K side with an RCCL-shaped cohort (``profiles/r3_coresidency.md``: no stranded cohort in any
+configuration, with or without the cap).
 
 Values already in the environment win (``setdefault``), so a user can re-tune either knob.
 """
@@ -24,20 +31,16 @@ from __future__ import annotations
 import os
 
 N_CU_MI355X = 256
-# CUs kept free of stream-K workgroups, and RCCL channels per collective; an RCCL gfx950 channel
-# block is 256 threads, 21 KB LDS, <= 128 VGPRs, so several fit on one free CU
+# CUs kept free of stream-K workgroups (an RCCL gfx950 channel block is 256 threads, 21 KB LDS,
+# <= 128 VGPRs, so several fit on one free CU)
 STREAMK_RESERVE_CUS = 8
-RCCL_MAX_CHANNELS = 32
 
 
 def multi_gpu_env(world_size: int, n_cu: int = N_CU_MI355X) -> dict[str, str]:
     """The variables :func:`apply_multi_gpu_env` would set for a ``world_size``-rank job."""
     if world_size <= 1:
         return {}
-    return {
-        "TENSILE_STREAMK_MAX_CUS": str(n_cu - STREAMK_RESERVE_CUS),
-        "NCCL_MAX_NCHANNELS": str(RCCL_MAX_CHANNELS),
-    }
+    return {"TENSILE_STREAMK_MAX_CUS": str(n_cu - STREAMK_RESERVE_CUS)}
 
 
 def apply_multi_gpu_env(world_size: int | None = None, n_cu: int = N_CU_MI355X) -> dict[str, str]:

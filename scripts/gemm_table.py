@@ -41,6 +41,12 @@ def main(paths):
             pick = "g8"
         entries[key] = pick
         detail[key] = {n: round(v, 4) for n, v in med.items()}
+    # Pinned regardless of timing: the XL vocabulary head (N or K = 10000 at d_model 1600) on the
+    # cs336 gemm8 tail kernels, so the XL step runs no hipBLASLt stream-K kernel (rccl_env.py);
+    # profiles/r4_gemm_report_xl_b96.json has the times (lm fwd 1.25 vs 1.09 ms, lm dX 1.36 vs 1.58 ms)
+    for key in entries:
+        if key.startswith("('nt'") and ("(10000, 1600)" in key or "(1600, 10000)" in key):
+            entries[key] = "g8"
     # lt pins (hipBLASLt candidate index + kernel name per problem) from the first report that has them
     pins = []
     for p in paths:
@@ -55,7 +61,12 @@ def main(paths):
         have = {",".join(x.split(",", 6)[:6]) for x in pins}
         pins = pins + [x for x in old.get("lt_pins", []) if ",".join(x.split(",", 6)[:6]) not in have]
         sources = old["_meta"].get("sources", []) + sources
-    doc = {"_meta": {"sources": sources, "rule": "median ms over reports; blas unless beaten by > 3 %",
+    if merge:  # pins apply to the kept entries too
+        for key in entries:
+            if key.startswith("('nt'") and ("(10000, 1600)" in key or "(1600, 10000)" in key):
+                entries[key] = "g8"
+    doc = {"_meta": {"sources": sources, "rule": "median ms over reports; blas unless beaten by > 3 %; "
+                     "XL vocabulary head pinned to g8 (no stream-K kernel in the XL step)",
                      "median_ms": detail}, "entries": entries, "lt_pins": pins}
     with open(OUT, "w") as f:
         json.dump(doc, f, indent=1)

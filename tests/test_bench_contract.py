@@ -64,7 +64,7 @@ def test_bench_multirank_json(nproc, extra):
     for r in sw:
         assert r["ms"] > 0 and r["algbw_gbs"] > 0
         assert r["busbw_gbs"] == pytest.approx(r["algbw_gbs"] * 2 * (nproc - 1) / nproc, rel=0.01)
-    assert dd["coresidency_caps"] == {"TENSILE_STREAMK_MAX_CUS": "248", "NCCL_MAX_NCHANNELS": "32"}
+    assert dd["coresidency_caps"] == {"TENSILE_STREAMK_MAX_CUS": "248"}  # no RCCL channel cap (rccl_env.py)
     # per-rank CPU affinity
     assert [a["rank"] for a in dd["cpu_affinity"]] == list(range(nproc))
     assert all("cpus" in a and "pinned" in a for a in dd["cpu_affinity"])
