@@ -102,6 +102,7 @@ def main(argv=None):
     ap.add_argument("--causal", nargs="+", type=int, default=[1, 0])
     ap.add_argument("--impls", nargs="+", default=["hip_fa2", "torch_sdpa", "torch_naive"])
     ap.add_argument("--sweep", action="store_true", help="seq 128..65536 x d 16..128 x {bf16, fp32}, B=1 (reference sweep)")
+    ap.add_argument("--sweep-dtype", nargs="+", default=None, help="--sweep: only these dtypes (default bf16 fp32)")
     ap.add_argument("--leaderboard", action="store_true")
     ap.add_argument("--no-compile", action="store_true")
     ap.add_argument("--rep", type=int, default=50)
@@ -115,7 +116,7 @@ def main(argv=None):
     else:
         seqs = [2**i for i in range(7, 17)] if a.sweep else a.seq
         ds = [16, 32, 64, 128] if a.sweep else a.d
-        dts = ["bf16", "fp32"] if a.sweep else a.dtype
+        dts = (a.sweep_dtype or ["bf16", "fp32"]) if a.sweep else a.dtype
         for dt in dts:
             for d in ds:
                 for n in seqs:
