@@ -117,8 +117,9 @@ def parse(argv=None):
         "--ddp-sweep",
         default="auto",
         choices=["auto", "on", "off"],
-        help="N > 1 (auto): after the timed steps, the handout's DDP comparison -- naive / flat / per-parameter / "
-        "bucketed {1,10,100,1000} MB ms/step + comm wait, ZeRO-1 memory -- into the JSON's dist block (<= 60 s)",
+        help="N > 1 (auto: with RCCL): after the timed steps, the handout's DDP comparison -- naive / flat / "
+        "per-parameter / bucketed {1,10,100,1000} MB ms/step + comm wait, ZeRO-1 memory -- into the JSON's dist "
+        "block (<= 60 s)",
     )
     ap.add_argument("--ddp-sweep-batch", type=int, default=4, help="per-GPU batch of the DDP sweep")
     ap.add_argument(
@@ -461,7 +462,11 @@ def main(argv=None):
         out["dist"] = dist_diagnostics(ddp_model, comm_wait_ms, device, world)
         if world > 1 and args.comm_sweep_mb:
             out["dist"]["allreduce_sweep_fp32"] = comm_sweep(args.comm_sweep_mb, device, world)
-    if world > 1 and args.ddp_sweep != "off" and not zero:
+    # auto: with RCCL (the driver's multi-GPU runs); a gloo rehearsal stages every all-reduce through
+    # the host (minutes per variant at XL), so there it runs only when asked for (--ddp-sweep on)
+    run_sweep = args.ddp_sweep == "on" or (args.ddp_sweep == "auto" and dist.is_initialized()
+                                            and dist.get_backend() == "nccl")
+    if world > 1 and run_sweep and not zero:
         # the headline fields are final; free the timed model, then the bounded DDP-variant table
         del ddp_model, opt, model, batches, graphed
         if device.type == "cuda":

@@ -236,8 +236,13 @@ def sweep_variants(model_name: str, ctx: int, per_rank_batch: int, dev: torch.de
             torch.cuda.empty_cache()
         return [float(v) for v in t.tolist()]
 
+    def note(msg):
+        if rank == 0:
+            print(f"ddp sweep: {msg} ({time.perf_counter() - t_start:.1f} s)", file=__import__("sys").stderr, flush=True)
+
     for variant, bucket_mb in variants:
         row = {"variant": variant, "bucket_mb": bucket_mb}
+        note(f"{variant} {bucket_mb if bucket_mb is not None else ''}")
         if over_budget():
             row["skipped"] = "time budget"
         else:

@@ -120,6 +120,10 @@ def _pick(kind: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None,
     hit = _BEST.get(key)
     if hit is None:
         t = selection_table().get(str(key))
+        if t is None:
+            # the same problem with other leading dimensions (ZeRO flat buffers put a group's Wᵀ in a
+            # wider run: (2560, 20480) with ld 665360 on the 2.7b): the table's dense-layout pick
+            t = selection_table().get(str(_dense_key(key)))
         if t is not None and t in cands:
             _BEST[key] = t
             _BEST_TIMES[key] = {"table": t}
@@ -144,6 +148,16 @@ def _pick(kind: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None,
 
 
 _BEST_TIMES: dict = {}
+
+
+def _dense_key(key: tuple) -> tuple:
+    """``key`` with every operand's row stride set to its row length (unit column stride kept)."""
+    kind, ash, ast, bsh, bst, out = key
+
+    def dense(shape, stride):
+        return (shape[1], 1) if len(shape) == 2 and stride[-1] == 1 else stride
+
+    return (kind, ash, dense(ash, ast), bsh, dense(bsh, bst), out)
 
 
 def gemm_choices() -> dict:

@@ -19,7 +19,8 @@ def _run(nproc: int, *extra: str) -> list[dict]:
         sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
         "--master-addr", "127.0.0.1", f"--master-port={find_free_port()}",
         "bench.py", "--gpus", str(nproc), "--steps", "2", "--warmup", "1",
-        "--model", "tiny", "--ctx", "32", "--batch", "2", "--dtype", "fp32", "--comm-sweep-mb", "1", "4", *extra,
+        "--model", "tiny", "--ctx", "32", "--batch", "2", "--dtype", "fp32", "--comm-sweep-mb", "1", "4",
+        "--ddp-sweep", "on", *extra,
     ]
     env = dict(os.environ, CS336_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
     out = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)

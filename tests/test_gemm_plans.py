@@ -33,3 +33,16 @@ def test_gemm8_extents():
     assert gemm.gemm8_extents_ok(_meta(49152, 10000), _meta(1600, 10000))
     assert gemm.gemm8_extents_ok(_meta(49152, 1600), _meta(10000, 1600))
     assert not gemm.gemm8_extents_ok(_meta(4096, 1600), _meta(700000, 1600))
+
+
+def test_dense_key_matches_table_entry():
+    """A problem whose operands sit in wider buffers (ZeRO-1 flat buffers give a group's Wᵀ a row
+    stride of 665360 on the 2.7b) maps to the committed dense-layout entry."""
+    key = ("nt", (12288, 20480), (20480, 1), (2560, 20480), (665360, 1), None)
+    dense = gemm._dense_key(key)
+    assert dense == ("nt", (12288, 20480), (20480, 1), (2560, 20480), (20480, 1), None)
+    table = gemm.selection_table() if False else __import__("json").load(open(gemm.TABLE_FILE))["entries"]
+    assert str(dense) in table
+    for k in (("nt", (12288, 2560), (2560, 1), (2560, 2560), (10240, 1), None),
+              ("nt", (12288, 7680), (7680, 1), (2560, 7680), (10240, 1), None)):
+        assert str(gemm._dense_key(k)) in table
