@@ -10,3 +10,5 @@ timeout -k 10 200 env CS336_FA_BWD=2 CS336_LIB=cs336_systems/_native/variants/no
 timeout -k 10 200 env CS336_FA_BWD=0 python -u scripts/fa_ab.py > gpurun_out/r4/fa_ab_two.log 2>&1 || exit $?
 timeout -k 10 700 python -u -m cs336_systems.bench.flash --sweep --sweep-dtype bf16 \
   --json gpurun_out/r4/flash_sweep_bf16.json > gpurun_out/r4/flash_sweep_bf16.log 2>&1 || exit $?
+timeout -k 10 400 bash scripts/rehearse_multirank.sh --batch 8 --comm-sweep-mb 1 10 > gpurun_out/r4/rh_xl.log 2>&1 || exit $?
+timeout -k 10 400 bash scripts/rehearse_multirank.sh --model small --ctx 512 --batch 8 --ddp-sweep on --comm-sweep-mb 1 > gpurun_out/r4/rh_small_sweep.log 2>&1 || exit $?
