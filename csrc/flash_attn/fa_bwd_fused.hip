@@ -250,10 +250,16 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
       }
       // C: the next key block's K image, behind the whole block
       if (s == sbeg(kb) && kb + 1 < nkb) issue_k(kb + 1);
-      // D: this wave's dQ partial sums from the earlier key blocks
+      // D: this wave's dQ partial sums from the earlier key blocks (L2), loaded here so their latency
+      // runs under the S/dP work instead of in front of the dQ product
       const int kb_last = CAUSAL ? min((q0 + FBQ - 1) / FKB, nkb - 1) : nkb - 1;
       const bool first = kb == 0, last = kb == kb_last;
       const int qrow = q0 + 32 * qqt + l32;
+      float4 pp[4];
+      if (dqw && !first) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) pp[g4] = *reinterpret_cast<const float4*>(part + qrow * FD + 8 * g4);
+      }
       const bool do_prep = first && s + 1 < nqs;  // next slice's delta (first key block only)
 
       // F: S, dP, P, dS, dVᵀ, dKᵀ of this wave's group; dSᵀ into LDS
@@ -340,11 +346,6 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_kernel(const AttnBwdParam
       // (splitting it over all eight waves with a partial-tile hand-off through LDS, or reading all
       // fragments ahead of the MFMAs, measured slower: profiles/r3_fa_bwd_fused_ab.md)
       if (dqw) {
-        float4 pp[4];  // this wave's dQ partial sums from the earlier key blocks (L2)
-        if (!first) {
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) pp[g4] = *reinterpret_cast<const float4*>(part + qrow * FD + 8 * g4);
-        }
         const int ng = CAUSAL ? min(8, (q0 + FBQ - kbase) / 32) : 8;  // active groups: 0 .. ng-1
         const int nv = min(ng, (N - kbase) / 32);
         f32x16 dq = zero16();
