@@ -115,7 +115,8 @@ def gemm_roles(step, xf, M, d, f, L, V):
     t["lm fwd"] += (fwd[-1][1] - fwd[-1][0]) / 1e6
     names["lm fwd"] = fwd[-1][2]
     # fused SwiGLU FFN (gemm8 epilogue 2 in the step): per layer w2 dW, w2 dX(+gate bwd), then the rest
-    fused = any("gemm8_kernel<5, 2>" in k or "gemm8_kernel<4, 2>" in k or "gemm8_kernelILi5ELi2" in k for _, _, k in bwd)
+    # (kernel names carry the template args: gemm8_kernel<FN, EPI[, TAIL]>, demangled or not)
+    fused = any(re.search(r"gemm8_kernel(<\d, 2[,>]|ILi\dELi2E)", k) for _, _, k in bwd)
     order = (["w2 dW", "w2 dX", "w13 dX", "w13 dW", "o dX", "o dW", "qkv dX", "qkv dW"] if fused else
              ["w2 dX", "w2 dW", "w13 dX", "w13 dW", "o dX", "o dW", "qkv dX", "qkv dW"])
     # the lm-head weight gradient may be a gemm8w kernel too: then the first backward GEMM is lm dW
