@@ -45,6 +45,50 @@ METRIC = "tokens/sec/node GPT-2-XL bf16 DDP"
 BASELINE_VALUE = None  # the reference publishes no number
 
 
+def emit_result(out: dict, json_out: str | None) -> None:
+    """The ONE JSON result line (rank 0), also written to ``--json-out``."""
+    line = json.dumps(out)
+    print(line, flush=True)
+    if json_out:
+        with open(json_out, "w") as f:
+            f.write(line + "\n")
+
+
+class SweepWatchdog:
+    """Bounds the post-headline DDP sweep. The headline fields are final before the sweep starts; if a
+    variant stalls (a collective that never completes would otherwise sit until the process group's
+    600 s timeout aborts the job without a result line), the timer marks the sweep timed out, rank 0
+    prints the headline line, and every rank leaves with status 0 (``os._exit``: the main thread is
+    blocked in the stuck call). Each rank arms its own timer, so no collective is needed to stop."""
+
+    def __init__(self, out: dict, rank: int, json_out: str | None, limit_s: float):
+        import threading
+
+        self.out, self.rank, self.json_out, self.limit_s = out, rank, json_out, limit_s
+        self._lock = threading.Lock()
+        self._done = False
+        self._timer = threading.Timer(limit_s, self._fire)
+        self._timer.daemon = True
+        self._timer.start()
+
+    def cancel(self) -> None:
+        with self._lock:
+            self._done = True
+        self._timer.cancel()
+
+    def _fire(self) -> None:
+        with self._lock:
+            if self._done:
+                return
+            self._done = True
+        self.out.setdefault("dist", {})["ddp_sweep"] = {"error": f"timed out after {self.limit_s:g} s"}
+        if self.rank == 0:
+            log(f"DDP sweep exceeded {self.limit_s:g} s: reporting the headline result without it")
+            emit_result(self.out, self.json_out)
+        sys.stderr.flush()
+        os._exit(0)
+
+
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -122,6 +166,13 @@ def parse(argv=None):
         "block (<= 60 s)",
     )
     ap.add_argument("--ddp-sweep-batch", type=int, default=4, help="per-GPU batch of the DDP sweep")
+    ap.add_argument(
+        "--ddp-sweep-timeout",
+        type=float,
+        default=240.0,
+        help="wall-clock limit of the DDP sweep: past it every rank stops, rank 0 having printed the headline line "
+        "with the sweep marked timed out (a stuck collective never costs the headline result)",
+    )
     ap.add_argument(
         "--tunableop",
         default="auto",
@@ -478,12 +529,15 @@ def main(argv=None):
         # uses the cs336 kernels only (gemm8 / gemm8w take every projection shape of it)
         gemm_mode_saved = os.environ.get("CS336_GEMM")
         os.environ["CS336_GEMM"] = "hip" if device.type == "cuda" else gemm_mode_saved or "blas"
+        dog = SweepWatchdog(out, rank, args.json_out, args.ddp_sweep_timeout)
         try:
             sw = sweep_variants(args.model, args.ctx, args.ddp_sweep_batch, device, amp=amp, vocab=args.vocab)
+            dog.cancel()
             out["dist"]["ddp_variants"] = sw.pop("variants")
             out["dist"]["zero1_memory"] = sw.pop("zero1_memory")
             out["dist"]["ddp_sweep"] = sw
         except Exception as e:  # noqa: BLE001 - the sweep never costs the headline line
+            dog.cancel()
             out["dist"]["ddp_sweep"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         finally:
             if gemm_mode_saved is None:
@@ -504,14 +558,13 @@ def main(argv=None):
         with open(rep + ".lt.json", "w") as fh:  # autotuned hipBLASLt candidates (scripts/gemm_table.py pins)
             json.dump(sorted(torch.ops.cs336.lt_gemm_picks()), fh, indent=1)
     if rank == 0:
-        line = json.dumps(out)
-        print(line, flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as f:
-                f.write(line + "\n")
+        emit_result(out, args.json_out)
     if dist.is_initialized():
-        dist.barrier()
-        dist.destroy_process_group()
+        try:
+            dist.barrier()
+            dist.destroy_process_group()
+        except Exception as e:  # noqa: BLE001 - a peer already left (sweep watchdog); the result line is out
+            log(f"rank {rank}: teardown after the result line failed ({type(e).__name__}); exiting")
     return 0
 
 

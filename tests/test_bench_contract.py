@@ -86,6 +86,16 @@ def test_bench_multirank_json(nproc, extra):
         assert dd["wire_mb_total"] == pytest.approx(dd["bucket_mb"]["total"] / 2, rel=0.01)
 
 
+def test_bench_ddp_sweep_watchdog():
+    """A DDP sweep that outlives ``--ddp-sweep-timeout`` never costs the headline line: rank 0 prints it
+    with the sweep marked failed and the job exits 0."""
+    lines = _run(2, "--ddp-sweep-timeout", "0.05")
+    assert len(lines) == 1, lines
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert "error" in d["dist"]["ddp_sweep"] and "ddp_variants" not in d["dist"]
+
+
 def test_bench_self_launch_without_launcher():
     """``python bench.py --gpus 2`` with no torchrun and no WORLD_SIZE: bench.py launches the two
     ranks itself and reports n_gpus 2 (never a mislabeled 1-GPU number)."""
