@@ -3,6 +3,7 @@ env switches, one process per setting): BASELINE config 2 (B 4, H 16, N 4096, d 
 not), the XL step (B 24, H 25, N 512, d 64, causal) and the 2.7b step (B 12, H 32, N 1024, d 80).
 
     CS336_FA_DMA=0 python scripts/fa_ab.py ; CS336_FA_DMA=1 python scripts/fa_ab.py
+    FA_AB_SHAPES="1,1,8192,128,0;1,1,4096,128,0" FA_AB_DTYPE=fp32 python scripts/fa_ab.py   # other shapes
 """
 
 import json
@@ -17,12 +18,16 @@ from cs336_systems.utils.timing import do_bench  # noqa: E402
 
 SHAPES = [(4, 16, 4096, 64, True), (4, 16, 4096, 64, False), (4, 16, 4096, 128, True), (4, 16, 4096, 128, False),
           (24, 25, 512, 64, True), (12, 32, 1024, 80, True)]
-tag = {k: v for k, v in os.environ.items() if k.startswith("CS336_FA")}
+if os.environ.get("FA_AB_SHAPES"):
+    SHAPES = [tuple(int(x) for x in sh.split(",")) for sh in os.environ["FA_AB_SHAPES"].split(";") if sh]
+    SHAPES = [(B, H, N, D, bool(c)) for B, H, N, D, c in SHAPES]
+DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[os.environ.get("FA_AB_DTYPE", "bf16")]
+tag = {k: v for k, v in os.environ.items() if k.startswith("CS336_FA") or k == "FA_AB_DTYPE"}
 for B, H, N, D, causal in SHAPES:
     torch.manual_seed(0)
-    mk = lambda: torch.randn(B, N, H, D, device="cuda", dtype=torch.bfloat16).transpose(1, 2).requires_grad_(True)  # noqa: E731
+    mk = lambda: torch.randn(B, N, H, D, device="cuda", dtype=DT).transpose(1, 2).requires_grad_(True)  # noqa: E731
     q, k, v = mk(), mk(), mk()
-    do = torch.randn(B, H, N, D, device="cuda", dtype=torch.bfloat16)
+    do = torch.randn(B, H, N, D, device="cuda", dtype=DT)
     f = lambda: ops.FlashAttentionHIP.apply(q, k, v, causal)  # noqa: E731
     o = f()
     t_f = do_bench(f, quantiles=(0.5,))
