@@ -46,6 +46,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
   constexpr int LPT = BN * CPR / 256;
   static_assert(BN * CPR % 256 == 0, "staging rounds must be whole");
   constexpr int NDT = DP / 32;
+  // no register prefetch of the next tile at fp32 d128: it fits (no scratch) but measured 2-10 %
+  // slower on every fp32 d128 shape (profiles/r4_fa_fp32_prefetch.md)
   constexpr bool PREFETCH = !(F32 && D == 128);
   static_assert(!DMA || (!F32 && ROPE != 1), "LDS-DMA staging: 16-bit, no RoPE-on-load");
   constexpr int NS = DMA ? 3 : 2;  // K/V ring depth
@@ -363,7 +365,7 @@ __global__ __launch_bounds__(256, (dkdv_min_waves<T, D>())) void fa_bwd_dkdv_ker
   constexpr int LPT = BQ * CPR / 256;
   static_assert(BQ * CPR % 256 == 0, "staging rounds must be whole");
   constexpr int NDT = DP / 32;
-  constexpr bool PREFETCH = !(F32 && D == 128);
+  constexpr bool PREFETCH = !(F32 && D == 128);  // see fa_bwd_dq_kernel
   static_assert(!DMA || (!F32 && ROPE != 1), "LDS-DMA staging: 16-bit, no RoPE-on-load");
   // LDS-DMA slot: Q, dO images, then L and delta in 1 KB regions (one wave-instruction each)
   constexpr int BUFD = 2 * TILE + 2048;
