@@ -252,12 +252,44 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
   //          kernel (fa_bwd_kp.hip, dQ by fp32 atomics), else the two-kernel form (split over keys /
   //          queries at low parallelism);
   //   1: head-sequential wherever it applies (then as unset); 2: key-block parallel wherever it
-  //   applies; 0: the two-kernel form (dQ kernel + dK/dV kernel: deterministic, any shape).
+  //   applies; 0: the two-kernel form (dQ kernel + dK/dV kernel: deterministic, any shape);
+  //   3: the two-workgroups-per-CU head-sequential kernel (fa_bwd_hs.hip) where it applies.
   const int mode = [] {
     const char* e = std::getenv("CS336_FA_BWD");
     return e && *e ? std::atoi(e) : -1;
   }();
   const int64_t nbh = q.size(0) * q.size(1);
+  // inverse RoPE of d(q|k) as one in-place pass after a kernel that returned them w.r.t. the rotated
+  // inputs (dq and dk adjacent head blocks of one buffer -- the fused dQKV layout -- take one launch)
+  auto rope_after_pass = [&]() {
+    const int64_t es = dq.element_size();
+    if (dk.strides() == dq.strides() &&
+        static_cast<const char*>(dk.data_ptr()) == static_cast<const char*>(dq.data_ptr()) + dq.size(1) * dq.stride(1) * es) {
+      const at::Tensor dqk = dq.as_strided({dq.size(0), 2 * dq.size(1), dq.size(2), dq.size(3)}, dq.strides());
+      rope_into(dqk, *rope_cos, *rope_sin, rope_pos, true, dqk);
+    } else {
+      rope_into(dq, *rope_cos, *rope_sin, rope_pos, true, dq);
+      rope_into(dk, *rope_cos, *rope_sin, rope_pos, true, dk);
+    }
+  };
+  // head-sequential with two 4-wave workgroups per CU (fa_bwd_hs.hip): mode 3. The inverse RoPE is
+  // folded into its dQ / dK stores unless CS336_FA_HS_ROPE=0 (then the separate pass above)
+  if (mode == 3) {
+    const char* re = std::getenv("CS336_FA_HS_ROPE");
+    const bool rope_after = bp.f.rope_out_only && re && *re && std::atoi(re) == 0;
+    cs336::AttnBwdParams hb = bp;
+    if (rope_after) {
+      hb.f.rope_cos = hb.f.rope_sin = nullptr;
+      hb.f.rope_pos = nullptr;
+      hb.f.rope_out_only = false;
+    }
+    if (cs336::flash_attn_bwd_hs_ok(hb, to_dtype(q))) {
+      at::Tensor ws = at::empty({(int64_t)cs336::flash_attn_bwd_hs_workspace(hb)}, q.options().dtype(at::kFloat));
+      cs336::flash_attn_bwd_hs(hb, to_dtype(q), ws.data_ptr<float>(), stream());
+      if (rope_after) rope_after_pass();
+      return;
+    }
+  }
   at::Tensor dq_acc;
   if (mode != 0 && mode != 2 && (mode == 1 || nbh >= 512)) {
     // partial sums exist only for rows with more than one 256-key block
@@ -275,19 +307,7 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
     }
     if (cs336::flash_attn_bwd_fused_ok(fb, to_dtype(q))) {
       cs336::flash_attn_bwd_fused(fb, to_dtype(q), stream());
-      if (rope_after) {
-        // dq and dk adjacent head blocks of one buffer (the fused dQKV layout): one launch over both
-        const int64_t es = dq.element_size();
-        if (dk.strides() == dq.strides() &&
-            static_cast<const char*>(dk.data_ptr()) ==
-                static_cast<const char*>(dq.data_ptr()) + dq.size(1) * dq.stride(1) * es) {
-          const at::Tensor dqk = dq.as_strided({dq.size(0), 2 * dq.size(1), dq.size(2), dq.size(3)}, dq.strides());
-          rope_into(dqk, *rope_cos, *rope_sin, rope_pos, true, dqk);
-        } else {
-          rope_into(dq, *rope_cos, *rope_sin, rope_pos, true, dq);
-          rope_into(dk, *rope_cos, *rope_sin, rope_pos, true, dk);
-        }
-      }
+      if (rope_after) rope_after_pass();
       return;
     }
     bp.dq_acc = nullptr;

@@ -196,5 +196,10 @@ void flash_attn_bwd_fused(const AttnBwdParams& p, DType t, hipStream_t s);
 bool flash_attn_bwd_kp_ok(const AttnBwdParams& p, DType t);
 size_t flash_attn_bwd_kp_workspace(const AttnBwdParams& p);
 void flash_attn_bwd_kp(const AttnBwdParams& p, DType t, float* ws, hipStream_t s);
+// one-kernel backward, one 4-wave workgroup per (batch, head) over 128-key blocks, two workgroups per
+// CU (fa_bwd_hs.hip): 16-bit, d 64, Nq == Nk, N % 128 == 0; ws = flash_attn_bwd_hs_workspace(p) floats
+bool flash_attn_bwd_hs_ok(const AttnBwdParams& p, DType t);
+size_t flash_attn_bwd_hs_workspace(const AttnBwdParams& p);
+void flash_attn_bwd_hs(const AttnBwdParams& p, DType t, float* ws, hipStream_t s);
 
 }  // namespace cs336

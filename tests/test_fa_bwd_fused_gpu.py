@@ -163,3 +163,51 @@ def test_kp_rope_out_only_in_step_layout(D, monkeypatch):
     monkeypatch.setenv("CS336_FA_BWD", "0")
     two = run()
     torch.testing.assert_close(kp.float(), two.float(), rtol=2e-2, atol=2e-2)
+
+
+# ---- head-sequential backward, two 4-wave workgroups per CU (csrc/flash_attn/fa_bwd_hs.hip) ----
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("N", [128, 256, 384, 512, 1024, 2048])
+def test_hs_bwd_vs_fp64(dt, causal, N, monkeypatch):
+    monkeypatch.setenv("CS336_FA_BWD", "3")
+    B, H = 2, 3
+    q, k, v, do = _inputs(B, H, N, dt)
+    hip = _hip()
+    o, lse = hip.fa_fwd(q, k, v, causal, 0.125)
+    dq, dk, dv = hip.fa_bwd(do, q, k, v, o, lse, causal, 0.125)
+    again = hip.fa_bwd(do, q, k, v, o, lse, causal, 0.125)
+    rq, rk, rv = _ref(q, k, v, do, causal)
+    for a, b, c, name in ((dq, rq, again[0], "dq"), (dk, rk, again[1], "dk"), (dv, rv, again[2], "dv")):
+        assert torch.equal(a, c), name  # deterministic: no atomics
+        err = (a.double() - b).abs().max().item()
+        scale = b.abs().max().item()
+        assert err <= 2e-2 * max(1.0, scale), f"{name}: max err {err} (ref max {scale})"
+
+
+@pytest.mark.parametrize("rope_in_kernel", ["1", "0"])
+def test_hs_rope_out_only_in_step_layout(rope_in_kernel, monkeypatch):
+    """The XL step's call through the two-workgroups-per-CU kernel: strided views of one fused
+    d(qkv) buffer, q/k already rotated, the inverse RoPE in the dQ / dK stores (or the separate pass)."""
+    B, H, N, D = 6, 25, 512, 64
+    torch.manual_seed(5)
+    qkv = torch.randn(B, N, 3, H, D, device=DEV, dtype=torch.bfloat16)
+    q, k, v = qkv[:, :, 0].transpose(1, 2), qkv[:, :, 1].transpose(1, 2), qkv[:, :, 2].transpose(1, 2)
+    do = torch.randn(B, N, H, D, device=DEV, dtype=torch.bfloat16).transpose(1, 2)
+    re = RotaryEmbedding(1024, D, 10000.0).to(DEV)
+    cos, sin = re.cos.contiguous(), re.sin.contiguous()
+    hip = _hip()
+    o, lse = hip.fa_fwd(q, k, v, True, D**-0.5)
+
+    def run():
+        d = torch.empty(B, N, 3, H, D, device=DEV, dtype=torch.bfloat16)
+        dq, dk, dv = d[:, :, 0].transpose(1, 2), d[:, :, 1].transpose(1, 2), d[:, :, 2].transpose(1, 2)
+        hip.fa_bwd_into(do, q, k, v, o, lse, True, D**-0.5, dq, dk, dv, cos, sin, None, True)
+        return d
+
+    monkeypatch.setenv("CS336_FA_HS_ROPE", rope_in_kernel)
+    monkeypatch.setenv("CS336_FA_BWD", "3")
+    hs = run()
+    monkeypatch.setenv("CS336_FA_BWD", "0")
+    two = run()
+    torch.testing.assert_close(hs.float(), two.float(), rtol=2e-2, atol=2e-2)

@@ -13,7 +13,8 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = "/opt/rocm/bin/hipcc"
 SOURCES = ["csrc/gemm/gemm8.hip", "csrc/gemm/gemm8w.hip", "csrc/flash_attn/fa_bwd_kp.hip",
-           "csrc/flash_attn/fa_bwd_fused.hip", "csrc/flash_attn/fa_fwd.hip"]
+           "csrc/flash_attn/fa_bwd_fused.hip", "csrc/flash_attn/fa_fwd.hip",
+           "csrc/flash_attn/fa_bwd_hs.hip"]
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="needs hipcc")
