@@ -247,8 +247,9 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
   bp.dk_sb = dk.stride(0); bp.dk_sh = dk.stride(1); bp.dk_sn = dk.stride(2);
   bp.dv_sb = dv.stride(0); bp.dv_sh = dv.stride(1); bp.dv_sn = dv.stride(2);
   // CS336_FA_BWD selects the backward:
-  //   unset: the head-sequential fused kernel (fa_bwd_fused.hip) where it applies and the (batch,
-  //          head) workgroups fill the chip (B·H >= 512), else at d 80 the key-block-parallel fused
+  //   unset: a head-sequential kernel where it applies and the (batch, head) workgroups fill the chip
+  //          (B·H >= 512): fa_bwd_hs.hip (d 64, N <= 1024, N % 128 == 0), else fa_bwd_fused.hip
+  //          (d 64, N <= 1024); else at d 80 the key-block-parallel fused
   //          kernel (fa_bwd_kp.hip, dQ by fp32 atomics), else the two-kernel form (split over keys /
   //          queries at low parallelism);
   //   1: head-sequential wherever it applies (then as unset); 2: key-block parallel wherever it
@@ -272,11 +273,13 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
       rope_into(dk, *rope_cos, *rope_sin, rope_pos, true, dk);
     }
   };
-  // head-sequential with two 4-wave workgroups per CU (fa_bwd_hs.hip): mode 3. The inverse RoPE is
-  // folded into its dQ / dK stores unless CS336_FA_HS_ROPE=0 (then the separate pass above)
-  if (mode == 3) {
+  // head-sequential with two 4-wave workgroups per CU (fa_bwd_hs.hip): mode 3, and by default for
+  // the training step's regime (B·H >= 512, N <= 1024), where it beat the 8-wave fused kernel in the
+  // XL step by 2.5-4.3 ms/step on two boxes (profiles/r4_fa_bwd_hs.md). The inverse RoPE runs as the
+  // separate pass after it (1.7-3.5 ms/step faster than in its stores) unless CS336_FA_HS_ROPE=1
+  if (mode == 3 || (mode < 0 && nbh >= 512 && q.size(2) <= 1024)) {
     const char* re = std::getenv("CS336_FA_HS_ROPE");
-    const bool rope_after = bp.f.rope_out_only && re && *re && std::atoi(re) == 0;
+    const bool rope_after = bp.f.rope_out_only && !(re && *re && std::atoi(re) == 1);
     cs336::AttnBwdParams hb = bp;
     if (rope_after) {
       hb.f.rope_cos = hb.f.rope_sin = nullptr;

@@ -173,6 +173,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
     const int key = kb * HS_KB + 32 * wave + l32;
 #pragma unroll
     for (int i = 0; i < 4; ++i) vf[i] = *reinterpret_cast<const uint4*>(Vp + key * v_sn + 16 * i + 8 * hh);
+  };
+  auto zero_kv = [&]() {
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
       dk[dt] = zero16();
@@ -212,6 +214,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
     if (kb1 < nkb) issue_slot(s1, 1);
   }
   load_v(0);
+  zero_kv();
   wait_vmcnt<0>();
   dma_barrier();
 
@@ -308,6 +311,18 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
           }
         }
       }
+      // the dQ store's RoPE coefficients (row qrow, pairs of d 32dqt + 8g4 + 4hh ..), loaded ahead of the
+      // barrier so their L2 latency runs under it and the dQ product
+      float2 rcs[4], rsn[4];
+      if (ROPE && last) {
+        const int64_t pos = bp.f.rope_pos ? bp.f.rope_pos[(int64_t)b * N + qrow] : qrow;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int64_t o = pos * (HS_D / 2) + 16 * dqt + 4 * g4 + 2 * hh;
+          rcs[g4] = *reinterpret_cast<const float2*>(rope.cs + o);
+          rsn[g4] = *reinterpret_cast<const float2*>(rope.sn + o);
+        }
+      }
       dma_barrier();  // D: dSᵀ of every group written, every wave done with this slot
 
       // E: dQᵀ tile = Kᵀ dSᵀ over the active groups (+ the earlier blocks' partial sums)
@@ -339,9 +354,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
             v1 *= sc;
             v2 *= sc;
             v3 *= sc;
-            if constexpr (ROPE) {
-              const int64_t pos = bp.f.rope_pos ? bp.f.rope_pos[(int64_t)b * N + qrow] : qrow;
-              rope_inv4(v0, v1, v2, v3, rope, pos, d);
+            if constexpr (ROPE) {  // R(pos)ᵀ on the pairs (d, d+1), (d+2, d+3)
+              const float2 c = rcs[g4], sn = rsn[g4];
+              const float a0 = c.x * v0 + sn.x * v1, a1 = -sn.x * v0 + c.x * v1;
+              const float b0 = c.y * v2 + sn.y * v3, b1 = -sn.y * v2 + c.y * v3;
+              v0 = a0; v1 = a1; v2 = b0; v3 = b1;
             }
             store4<T>(dQp + (int64_t)qrow * bp.dq_sn + d, make_float4(v0, v1, v2, v3));
           } else {
@@ -362,12 +379,16 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
       }
       nwait = 4 + ndma;
     }
-    // H: this key block's dK, dV; the next block's K image and V (drain)
-    store_kv(kb);
+    // H: the next block's K image and V in flight first, then this block's dK, dV stores (the wait
+    // for their RoPE coefficient loads also covers those), then drain
     if (kb + 1 < nkb) {
       dma_barrier();  // every wave done reading the K image
       dk_.issue(Kp + (int64_t)(kb + 1) * HS_KB * k_sn, HS_KB, k_sn, Kimg, wave);
       load_v(kb + 1);
+    }
+    store_kv(kb);
+    if (kb + 1 < nkb) {
+      zero_kv();
       wait_vmcnt<0>();
       dma_barrier();
       nwait = 63;

@@ -18,7 +18,7 @@ for f in glob.glob(f"gpurun_out/pmc_{tag}/p*/**/*counter_collection.csv", recurs
     vals = {}
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        k = "dq" if "fa_bwd_dq" in n else ("dkdv" if "fa_bwd_dkdv" in n else ("fused" if "fa_bwd_fused" in n else None))
+        k = "dq" if "fa_bwd_dq" in n else ("dkdv" if "fa_bwd_dkdv" in n else ("fused" if "fa_bwd_fused" in n else ("hs" if "fa_bwd_hs_kernel" in n else ("hs_prep" if "fa_bwd_hs_prep" in n else None))))
         if not k: continue
         vals.setdefault((k, r["Counter_Name"]), {}).setdefault(r["Dispatch_Id"], 0.0)
         vals[(k, r["Counter_Name"])][r["Dispatch_Id"]] += float(r["Counter_Value"])
@@ -28,7 +28,7 @@ for f in glob.glob(f"gpurun_out/pmc_{tag}/kt/**/*kernel_trace.csv", recursive=Tr
     ts = {}
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        k = "dq" if "fa_bwd_dq" in n else ("dkdv" if "fa_bwd_dkdv" in n else ("fused" if "fa_bwd_fused" in n else None))
+        k = "dq" if "fa_bwd_dq" in n else ("dkdv" if "fa_bwd_dkdv" in n else ("fused" if "fa_bwd_fused" in n else ("hs" if "fa_bwd_hs_kernel" in n else ("hs_prep" if "fa_bwd_hs_prep" in n else None))))
         if k: ts.setdefault(k, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     for k, v in ts.items():
         res.setdefault(k, {})["duration_us_median"] = statistics.median(v)

@@ -1,6 +1,7 @@
-"""The fused one-kernel FlashAttention-2 backward (csrc/flash_attn/fa_bwd_fused.hip: one workgroup
-per (batch, head), five MFMA products per tile, dQ summed across key blocks through fp32 partials)
-against an fp64 reference, the two-kernel backward, and the default selection (fused at B·H >= 512)."""
+"""The one-kernel FlashAttention-2 backwards (csrc/flash_attn/fa_bwd_fused.hip: one 8-wave workgroup
+per (batch, head); fa_bwd_hs.hip: one 4-wave workgroup per (batch, head), two per CU; fa_bwd_kp.hip:
+one workgroup per key block, dQ by atomics) against an fp64 reference, the two-kernel backward, and
+the default selection (head-sequential at B·H >= 512)."""
 
 import math
 
@@ -67,8 +68,9 @@ def test_fused_matches_two_kernel(causal, N, monkeypatch):
 
 def test_fused_rope_out_only_in_step_layout(monkeypatch):
     """The XL step's call: dq/dk/dv written into the three slices of one fused d(qkv) buffer, q/k
-    already rotated, inverse RoPE fused into the dQ/dK store; B·H = 600 >= 512 takes the fused
-    kernel by default (bitwise equal to forcing it)."""
+    already rotated, dq/dk returned w.r.t. the un-rotated inputs; B·H = 600 >= 512 takes the
+    head-sequential two-workgroups-per-CU kernel by default (bitwise equal to forcing it), and the
+    8-wave fused kernel agrees with the two-kernel form."""
     B, H, N, D = 24, 25, 512, 64
     torch.manual_seed(2)
     qkv = torch.randn(B, N, 3, H, D, device=DEV, dtype=torch.bfloat16)
@@ -86,13 +88,17 @@ def test_fused_rope_out_only_in_step_layout(monkeypatch):
         return d
 
     monkeypatch.delenv("CS336_FA_BWD", raising=False)
+    monkeypatch.delenv("CS336_FA_HS_ROPE", raising=False)
     default = run()
+    monkeypatch.setenv("CS336_FA_BWD", "3")
+    hs = run()
     monkeypatch.setenv("CS336_FA_BWD", "1")
     fused = run()
     monkeypatch.setenv("CS336_FA_BWD", "0")
     two = run()
-    assert torch.equal(default, fused)
+    assert torch.equal(default, hs)
     torch.testing.assert_close(fused.float(), two.float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(hs.float(), two.float(), rtol=2e-2, atol=2e-2)
 
 
 # ---- key-block-parallel fused backward (csrc/flash_attn/fa_bwd_kp.hip, dQ by fp32 atomics) ----
