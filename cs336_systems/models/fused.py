@@ -533,8 +533,11 @@ class FusedLinearFn(torch.autograd.Function):
                 dx = dx.to(ctx.x_dtype)
         if any(ctx.needs_input_grad[1:]):
             target = FusedLinearFn._grad_target(ctx.weights) if dy2.dtype == torch.bfloat16 else None
+            g8w = getattr(ctx, "dw_g8w", False) and gemm.dw_g8w_ok(dy2, x2)
             # side stream only when the grads are unset: AccumulateGrad then adopts dW without a
-            # kernel (an accumulate-add on the main stream would race the side-stream GEMM)
+            # kernel (an accumulate-add on the main stream would race the side-stream GEMM); and only
+            # for a data-parallel cs336 kernel (gemm8w, or the cs336 GEMM): never a stream-K GEMM
+            # beside another GEMM
             side = (
                 dy2.is_cuda
                 and dy2.dtype == torch.bfloat16
@@ -542,10 +545,9 @@ class FusedLinearFn(torch.autograd.Function):
                 and dw_stream_enabled()
                 and all(p.grad is None for p in ctx.weights)
                 and all(dt == torch.float32 for dt in ctx.wdtype)
-                and gemm.dw_concurrent_ok(dy2, x2, ctx.xt)  # never a stream-K GEMM beside another GEMM
+                and (g8w or gemm.dw_concurrent_ok(dy2, x2, ctx.xt))
             )
             dyt = None
-            g8w = getattr(ctx, "dw_g8w", False) and not side and gemm.dw_g8w_ok(dy2, x2)
             if g8w:
                 take_transposed_grad(dy2)  # drop a producer's dYᵀ offer: not needed
             elif not side and dy2.is_cuda and dy2.dtype == torch.bfloat16 and _dy_transposed(ctx.x_shape[-1], dy2.shape[1]):

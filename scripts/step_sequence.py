@@ -28,8 +28,10 @@ def main():
     lo, hi = starts[-2], starts[-1]
     step = [x for x in iv if lo <= x[0] < hi]
     fwd_fa = [i for i, x in enumerate(step) if "fa_fwd" in x[2]]
-    # one FA backward kernel per layer: the fused form, or the dQ kernel of the two-kernel form
-    bwd_fa = [i for i, x in enumerate(step) if "fa_bwd_dq" in x[2] or "fa_bwd_fused" in x[2]]
+    # one FA backward anchor per layer: the fused forms' first launch (the hs / kp prep kernel), or
+    # the dQ kernel of the two-kernel form
+    anchors = ("fa_bwd_dq", "fa_bwd_fused", "fa_bwd_hs_prep", "fa_bwd_kp_prep")
+    bwd_fa = [i for i, x in enumerate(step) if any(a in x[2] for a in anchors)]
     L = a.layer
     print(f"== forward, layer {L}")
     for x in step[fwd_fa[L]:fwd_fa[L + 1]]:
