@@ -276,20 +276,24 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
   // head-sequential with two 4-wave workgroups per CU (fa_bwd_hs.hip): mode 3, and by default for
   // the training step's regime (B·H >= 512, N <= 1024), where it beat the 8-wave fused kernel in the
   // XL step by 2.5-4.3 ms/step on two boxes (profiles/r4_fa_bwd_hs.md). The inverse RoPE runs as the
-  // separate pass after it (1.7-3.5 ms/step faster than in its stores) unless CS336_FA_HS_ROPE=1
+  // separate pass after it (1.7-3.5 ms/step faster than in its stores). CS336_FA_HS_ROPE: 0 (default)
+  // both dQ and dK by the pass, 1 both in the kernel's stores, 2 dK in the kernel (at the key-block
+  // switch, where it drains anyway) and dQ by the pass
   if (mode == 3 || (mode < 0 && nbh >= 512 && q.size(2) <= 1024)) {
     const char* re = std::getenv("CS336_FA_HS_ROPE");
-    const bool rope_after = bp.f.rope_out_only && !(re && *re && std::atoi(re) == 1);
+    const int hr = re && *re ? std::atoi(re) : 0;
+    const bool rope = bp.f.rope_out_only;
     cs336::AttnBwdParams hb = bp;
-    if (rope_after) {
+    if (rope && hr == 0) {
       hb.f.rope_cos = hb.f.rope_sin = nullptr;
       hb.f.rope_pos = nullptr;
       hb.f.rope_out_only = false;
     }
     if (cs336::flash_attn_bwd_hs_ok(hb, to_dtype(q))) {
       at::Tensor ws = at::empty({(int64_t)cs336::flash_attn_bwd_hs_workspace(hb)}, q.options().dtype(at::kFloat));
-      cs336::flash_attn_bwd_hs(hb, to_dtype(q), ws.data_ptr<float>(), stream());
-      if (rope_after) rope_after_pass();
+      cs336::flash_attn_bwd_hs(hb, to_dtype(q), ws.data_ptr<float>(), stream(), hr != 2);
+      if (rope && hr == 0) rope_after_pass();
+      if (rope && hr == 2) rope_into(dq, *rope_cos, *rope_sin, rope_pos, true, dq);
       return;
     }
   }

@@ -96,7 +96,9 @@ __global__ __launch_bounds__(256) void fa_bwd_hs_prep(const AttnBwdParams bp, fl
 }
 
 // ---- (2) main kernel -------------------------------------------------------------------------
-template <typename T, bool CAUSAL, bool ROPE>
+// ROPE: 0 = none, 1 = inverse rotation in the dQ and dK stores, 2 = in the dK stores only (the caller
+// rotates dQ back in a separate pass)
+template <typename T, bool CAUSAL, int ROPE>
 __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams bp, const float* __restrict__ rowc,
                                                            float* __restrict__ part_all) {
   typedef typename Elem<T>::storage S;
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
     const int key = kb * HS_KB + 32 * wave + l32;
     S* rk = (S*)bp.dk + b * bp.dk_sb + h * bp.dk_sh + (int64_t)key * bp.dk_sn;
     S* rv = (S*)bp.dv + b * bp.dv_sb + h * bp.dv_sh + (int64_t)key * bp.dv_sn;
-    const int64_t pos = ROPE ? (bp.f.rope_pos ? bp.f.rope_pos[(int64_t)b * N + key] : key) : 0;
+    const int64_t pos = ROPE != 0 ? (bp.f.rope_pos ? bp.f.rope_pos[(int64_t)b * N + key] : key) : 0;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
         const int d = 32 * dt + 8 * g4 + 4 * hh;
         float k0 = dk[dt][4 * g4] * sc, k1 = dk[dt][4 * g4 + 1] * sc, k2 = dk[dt][4 * g4 + 2] * sc,
               k3 = dk[dt][4 * g4 + 3] * sc;
-        if constexpr (ROPE) rope_inv4(k0, k1, k2, k3, rope, pos, d);
+        if constexpr (ROPE != 0) rope_inv4(k0, k1, k2, k3, rope, pos, d);
         store4<T>(rk + d, make_float4(k0, k1, k2, k3));
         store4<T>(rv + d, make_float4(dv[dt][4 * g4], dv[dt][4 * g4 + 1], dv[dt][4 * g4 + 2], dv[dt][4 * g4 + 3]));
       }
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
       // the dQ store's RoPE coefficients (row qrow, pairs of d 32dqt + 8g4 + 4hh ..), loaded ahead of the
       // barrier so their L2 latency runs under it and the dQ product
       float2 rcs[4], rsn[4];
-      if (ROPE && last) {
+      if (ROPE == 1 && last) {
         const int64_t pos = bp.f.rope_pos ? bp.f.rope_pos[(int64_t)b * N + qrow] : qrow;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
@@ -354,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
             v1 *= sc;
             v2 *= sc;
             v3 *= sc;
-            if constexpr (ROPE) {  // R(pos)ᵀ on the pairs (d, d+1), (d+2, d+3)
+            if constexpr (ROPE == 1) {  // R(pos)ᵀ on the pairs (d, d+1), (d+2, d+3)
               const float2 c = rcs[g4], sn = rsn[g4];
               const float a0 = c.x * v0 + sn.x * v1, a1 = -sn.x * v0 + c.x * v1;
               const float b0 = c.y * v2 + sn.y * v3, b1 = -sn.y * v2 + c.y * v3;
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
   }
 }
 
-template <typename T, bool C, bool R>
+template <typename T, bool C, int R>
 void launch_hs(const AttnBwdParams& bp, float* rowc, float* part, hipStream_t s) {
   const int BH = bp.f.B * bp.f.H, N = bp.f.Nq;
   hipLaunchKernelGGL((fa_bwd_hs_prep<T>), dim3((unsigned)(BH * (N / HS_BQ))), dim3(256), 0, s, bp, rowc);
@@ -404,14 +406,16 @@ void launch_hs(const AttnBwdParams& bp, float* rowc, float* part, hipStream_t s)
 }
 
 template <typename T>
-void dispatch_hs(const AttnBwdParams& bp, float* rowc, float* part, hipStream_t s) {
-  const bool rope = bp.f.rope_cos != nullptr;
+void dispatch_hs(const AttnBwdParams& bp, float* rowc, float* part, bool rope_dq, hipStream_t s) {
+  const int rope = bp.f.rope_cos == nullptr ? 0 : (rope_dq ? 1 : 2);
   if (bp.f.causal) {
-    if (rope) launch_hs<T, true, true>(bp, rowc, part, s);
-    else launch_hs<T, true, false>(bp, rowc, part, s);
+    if (rope == 1) launch_hs<T, true, 1>(bp, rowc, part, s);
+    else if (rope == 2) launch_hs<T, true, 2>(bp, rowc, part, s);
+    else launch_hs<T, true, 0>(bp, rowc, part, s);
   } else {
-    if (rope) launch_hs<T, false, true>(bp, rowc, part, s);
-    else launch_hs<T, false, false>(bp, rowc, part, s);
+    if (rope == 1) launch_hs<T, false, 1>(bp, rowc, part, s);
+    else if (rope == 2) launch_hs<T, false, 2>(bp, rowc, part, s);
+    else launch_hs<T, false, 0>(bp, rowc, part, s);
   }
 }
 
@@ -435,12 +439,12 @@ size_t flash_attn_bwd_hs_workspace(const AttnBwdParams& bp) {
   return rows * 2 + (bp.f.Nq > fa::HS_KB ? rows * fa::HS_D : 4);  // floats: row constants + dQ partials
 }
 
-void flash_attn_bwd_hs(const AttnBwdParams& bp, DType t, float* ws, hipStream_t s) {
+void flash_attn_bwd_hs(const AttnBwdParams& bp, DType t, float* ws, hipStream_t s, bool rope_dq) {
   if (bp.f.B * bp.f.H == 0) return;
   float* rowc = ws;
   float* part = ws + (size_t)bp.f.B * bp.f.H * bp.f.Nq * 2;
-  if (t == DType::BF16) fa::dispatch_hs<BF16>(bp, rowc, part, s);
-  else fa::dispatch_hs<F16>(bp, rowc, part, s);
+  if (t == DType::BF16) fa::dispatch_hs<BF16>(bp, rowc, part, rope_dq, s);
+  else fa::dispatch_hs<F16>(bp, rowc, part, rope_dq, s);
 }
 
 }  // namespace cs336

@@ -200,6 +200,7 @@ void flash_attn_bwd_kp(const AttnBwdParams& p, DType t, float* ws, hipStream_t s
 // CU (fa_bwd_hs.hip): 16-bit, d 64, Nq == Nk, N % 128 == 0; ws = flash_attn_bwd_hs_workspace(p) floats
 bool flash_attn_bwd_hs_ok(const AttnBwdParams& p, DType t);
 size_t flash_attn_bwd_hs_workspace(const AttnBwdParams& p);
-void flash_attn_bwd_hs(const AttnBwdParams& p, DType t, float* ws, hipStream_t s);
+// rope_dq = false (with RoPE): only dK is rotated back in the kernel; the caller rotates dQ
+void flash_attn_bwd_hs(const AttnBwdParams& p, DType t, float* ws, hipStream_t s, bool rope_dq = true);
 
 }  // namespace cs336

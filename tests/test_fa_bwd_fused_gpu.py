@@ -191,7 +191,7 @@ def test_hs_bwd_vs_fp64(dt, causal, N, monkeypatch):
         assert err <= 2e-2 * max(1.0, scale), f"{name}: max err {err} (ref max {scale})"
 
 
-@pytest.mark.parametrize("rope_in_kernel", ["1", "0"])
+@pytest.mark.parametrize("rope_in_kernel", ["1", "0", "2"])
 def test_hs_rope_out_only_in_step_layout(rope_in_kernel, monkeypatch):
     """The XL step's call through the two-workgroups-per-CU kernel: strided views of one fused
     d(qkv) buffer, q/k already rotated, the inverse RoPE in the dQ / dK stores (or the separate pass)."""
