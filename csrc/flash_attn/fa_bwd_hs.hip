@@ -51,7 +51,20 @@ constexpr int HS_OFF_K = HS_NS * HS_SLOT;
 constexpr int HS_OFF_DS = HS_OFF_K + HS_KB * HS_RB;
 constexpr int HS_LDS = HS_OFF_DS + HS_KB * 128;  // dSᵀ [key][64 q], 128-B rows
 static_assert(HS_LDS <= 80 * 1024, "two workgroups per CU");
+// in-kernel delta (IND): + an O slice image (single, restaged one item ahead) + -delta of the whole
+// head (fp32, row_perm order per slice), N <= HS_MAXN
+constexpr int HS_MAXN = 1024;
+constexpr int HS_OFF_O = HS_LDS;
+constexpr int HS_OFF_DH = HS_OFF_O + HS_TILE;
+constexpr int HS_LDS_IND = HS_OFF_DH + HS_MAXN * 4;
+static_assert(HS_LDS_IND <= 80 * 1024, "two workgroups per CU");
 constexpr int HS_SLICE_DMA = 2 * (HS_BQ * (HS_RB / 16) / 256);  // Q + dO wave-instructions per wave
+
+// CS336_FA_HS_DELTA=0: row constants from the prep kernel instead of the in-kernel delta
+inline bool hs_in_kernel_delta() {
+  const char* e = getenv("CS336_FA_HS_DELTA");
+  return !(e && *e && atoi(e) == 0);
+}
 
 // wait until at most n of this wave's vector memory operations are outstanding (n wave-uniform;
 // the counts that occur: 4 + {0, 4, 5})
@@ -97,13 +110,16 @@ __global__ __launch_bounds__(256) void fa_bwd_hs_prep(const AttnBwdParams bp, fl
 
 // ---- (2) main kernel -------------------------------------------------------------------------
 // ROPE: 0 = none, 1 = inverse rotation in the dQ and dK stores, 2 = in the dK stores only (the caller
-// rotates dQ back in a separate pass)
-template <typename T, bool CAUSAL, int ROPE>
+// rotates dQ back in a separate pass). IND: delta = rowsum(dO·O) computed here during the first key
+// block's pass (O slices staged by LDS-DMA one item ahead, -delta of the head kept in LDS) and the
+// row's lse staged raw with each slice -- no prep kernel, no second read of dO; else the row
+// constants come from fa_bwd_hs_prep (rowc).
+template <typename T, bool CAUSAL, int ROPE, bool IND>
 __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams bp, const float* __restrict__ rowc,
                                                            float* __restrict__ part_all) {
   typedef typename Elem<T>::storage S;
   typedef typename Mma16<T>::frag F;
-  __shared__ __attribute__((aligned(1024))) char smem[HS_LDS];
+  __shared__ __attribute__((aligned(1024))) char smem[IND ? HS_LDS_IND : HS_LDS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int l32 = lane & 31, hh = lane >> 5;
@@ -151,14 +167,45 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
   dd_.init(wave, lane, do_sn);
   TileDma<HS_KB, HS_RB, 8, 2> dk_;
   dk_.init(wave, lane, k_sn);
-  const __amdgpu_buffer_rsrc_t rrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(rowc + (int64_t)bh * nqs * 128), (short)0, nqs * 512, 0x00020000);
-  const uint32_t vrc = lane < 32 ? (uint32_t)(lane * 16) : 0x80000000u;  // lanes 32-63: out of range
+  // row constants of a slice: IND -- the slice's 64 raw lse values (256 B) in row_perm order, lane c < 16
+  // moving source rows 4 row_perm_src_chunk(c) .. +3; else 512 B of the prep kernel's rowc
+  const __amdgpu_buffer_rsrc_t rrc =
+      IND ? __builtin_amdgcn_make_buffer_rsrc((void*)(bp.f.lse + (int64_t)bh * N), (short)0, N * 4, 0x00020000)
+          : __builtin_amdgcn_make_buffer_rsrc((void*)(rowc + (int64_t)bh * nqs * 128), (short)0, nqs * 512, 0x00020000);
+  const uint32_t vrc = IND ? (lane < 16 ? (uint32_t)(row_perm_src_chunk(lane) * 16) : 0x80000000u)
+                           : (lane < 32 ? (uint32_t)(lane * 16) : 0x80000000u);  // other lanes: out of range
   auto issue_slot = [&](int s, int slot) {
     char* base = smem + slot * HS_SLOT;
     dq_.issue(Qp + (int64_t)s * HS_BQ * q_sn, HS_BQ, q_sn, base, wave);
     dd_.issue(dOp + (int64_t)s * HS_BQ * do_sn, HS_BQ, do_sn, base + HS_TILE, wave);
-    if (wave == 0) dma16(rrc, lds_addr(base + 2 * HS_TILE), vrc, (uint32_t)(s * 512));
+    if (wave == 0) dma16(rrc, lds_addr(base + 2 * HS_TILE), vrc, (uint32_t)(s * (IND ? 256 : 512)));
+  };
+  // IND: O slice image (single buffer) and the head's -delta
+  TileDma<HS_BQ, HS_RB, 8, 2> do_;
+  if constexpr (IND) do_.init(wave, lane, bp.f.o_sn);
+  const S* Op = (const S*)bp.f.o + b * bp.f.o_sb + h * bp.f.o_sh;
+  char* const Oimg = smem + HS_OFF_O;
+  float* const Dh = reinterpret_cast<float*>(smem + HS_OFF_DH);
+  auto issue_o = [&](int s) { do_.issue(Op + (int64_t)s * HS_BQ * bp.f.o_sn, HS_BQ, bp.f.o_sn, Oimg, wave); };
+  // -delta of slice s from the landed dO (slot image) and O images: thread = (row tid>>2, 16 d of
+  // quarter tid&3 = chunks 2k, 2k+1)
+  auto delta_slice = [&](int s, const char* dOs) {
+    const int r = tid >> 2, k = tid & 3;
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 2 * k; c < 2 * k + 2; ++c) {
+      const uint4 ug = *reinterpret_cast<const uint4*>(dOs + lds_off<HS_RB>(r, c));
+      const uint4 uo = *reinterpret_cast<const uint4*>(Oimg + lds_off<HS_RB>(r, c));
+      const uint32_t wg[4] = {ug.x, ug.y, ug.z, ug.w}, wo[4] = {uo.x, uo.y, uo.z, uo.w};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        acc = fmaf(Elem<T>::to_f((S)(wg[w] & 0xffff)), Elem<T>::to_f((S)(wo[w] & 0xffff)), acc);
+        acc = fmaf(Elem<T>::to_f((S)(wg[w] >> 16)), Elem<T>::to_f((S)(wo[w] >> 16)), acc);
+      }
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    if (k == 0) Dh[s * HS_BQ + row_perm(r)] = -acc;
   };
   auto sbeg = [&](int kb) { return CAUSAL ? kb * (HS_KB / HS_BQ) : 0; };
   auto advance = [&](int& kb, int& s) {
@@ -209,6 +256,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
 
   // ---- prologue: K image 0, slices of items 0 and 1, V of block 0 -----------------------------------
   dk_.issue(Kp, HS_KB, k_sn, Kimg, wave);
+  if constexpr (IND) issue_o(0);
   {
     int kb1 = 0, s1 = sbeg(0);
     issue_slot(s1, 0);
@@ -229,18 +277,29 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
       const int slot = it & 1;
       const char* Qs = smem + slot * HS_SLOT;
       const char* dOs = Qs + HS_TILE;
-      const float* Ls = reinterpret_cast<const float*>(Qs + 2 * HS_TILE);  // -lse·log2e, row_perm order
-      const float* Ds = Ls + 64;                                           // -delta
+      const float* Ls = reinterpret_cast<const float*>(Qs + 2 * HS_TILE);  // -lse·log2e (IND: lse), row_perm order
+      const float* Ds = IND ? Dh + s * HS_BQ : Ls + 64;                    // -delta
       const int q0 = s * HS_BQ;
       // A: this item's slice landed in every wave's share; the previous item's dSᵀ / K reads retired
       wait_vm_upto(nwait);
       dma_barrier();
+      if (IND && kb == 0) {
+        // the slice's -delta (first key block: every slice passes once), then the next O slice into
+        // the freed O image
+        delta_slice(s, dOs);
+        dma_barrier();
+        if (s + 1 < nqs) issue_o(s + 1);
+      }
       // B: this tile's dQ partial sums from the earlier key blocks (L2)
       const int kb_last = CAUSAL ? min((q0 + HS_BQ - 1) / HS_KB, nkb - 1) : nkb - 1;
       const bool first = kb == 0, last = kb == kb_last;
       const int qrow = q0 + 32 * qqt + l32;
       float4 pp[4];
+#ifdef CS336_HS_NO_PP  // A/B probe only (wrong dQ): the kernel's time without its dQ partial loads
+      if (false) {
+#else
       if (!first) {
+#endif
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) pp[g4] = *reinterpret_cast<const float4*>(part + qrow * HS_D + 8 * g4);
       }
@@ -274,7 +333,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
 #pragma unroll
           for (int g4 = 0; g4 < 4; ++g4) {
             const float4 L4 = *reinterpret_cast<const float4*>(Ls + 32 * t + 16 * hh + 4 * g4);
-            const float Lv[4] = {L4.x, L4.y, L4.z, L4.w};
+            const float lm = IND ? -kLog2e : 1.f;
+            const float Lv[4] = {lm * L4.x, lm * L4.y, lm * L4.z, lm * L4.w};
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               const int r = 4 * g4 + u;
@@ -344,7 +404,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           float v0 = dq[4 * g4], v1 = dq[4 * g4 + 1], v2 = dq[4 * g4 + 2], v3 = dq[4 * g4 + 3];
+#ifdef CS336_HS_NO_PP
+          if (false) {
+#else
           if (!first) {
+#endif
             v0 += pp[g4].x;
             v1 += pp[g4].y;
             v2 += pp[g4].z;
@@ -401,8 +465,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
 template <typename T, bool C, int R>
 void launch_hs(const AttnBwdParams& bp, float* rowc, float* part, hipStream_t s) {
   const int BH = bp.f.B * bp.f.H, N = bp.f.Nq;
+  if (N <= HS_MAXN && hs_in_kernel_delta()) {
+    hipLaunchKernelGGL((fa_bwd_hs_kernel<T, C, R, true>), dim3((unsigned)BH), dim3(256), 0, s, bp, rowc, part);
+    return;
+  }
   hipLaunchKernelGGL((fa_bwd_hs_prep<T>), dim3((unsigned)(BH * (N / HS_BQ))), dim3(256), 0, s, bp, rowc);
-  hipLaunchKernelGGL((fa_bwd_hs_kernel<T, C, R>), dim3((unsigned)BH), dim3(256), 0, s, bp, rowc, part);
+  hipLaunchKernelGGL((fa_bwd_hs_kernel<T, C, R, false>), dim3((unsigned)BH), dim3(256), 0, s, bp, rowc, part);
 }
 
 template <typename T>

@@ -217,3 +217,20 @@ def test_hs_rope_out_only_in_step_layout(rope_in_kernel, monkeypatch):
     monkeypatch.setenv("CS336_FA_BWD", "0")
     two = run()
     torch.testing.assert_close(hs.float(), two.float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("N", [128, 512, 1024])
+def test_hs_in_kernel_delta_matches_prep(causal, N, monkeypatch):
+    """fa_bwd_hs.hip computes delta = rowsum(dO·O) itself during the first key block (default for
+    N <= 1024) or takes it from the prep kernel (CS336_FA_HS_DELTA=0): same sums, bitwise equal."""
+    monkeypatch.setenv("CS336_FA_BWD", "3")
+    B, H = 3, 4
+    q, k, v, do = _inputs(B, H, N, torch.bfloat16, seed=6)
+    hip = _hip()
+    o, lse = hip.fa_fwd(q, k, v, causal, 0.125)
+    ind = hip.fa_bwd(do, q, k, v, o, lse, causal, 0.125)
+    monkeypatch.setenv("CS336_FA_HS_DELTA", "0")
+    prep = hip.fa_bwd(do, q, k, v, o, lse, causal, 0.125)
+    for a, b in zip(ind, prep):
+        assert torch.equal(a, b)
