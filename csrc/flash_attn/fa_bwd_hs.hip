@@ -306,7 +306,6 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
 
       // C: S, dP, P, dS, dVᵀ, dKᵀ of this wave's group; dSᵀ into LDS
       if (!CAUSAL || k0g <= q0 + HS_BQ - 1) {
-        const bool diag = CAUSAL && k0g + 31 > q0;
         const char* Kg = Kimg + 32 * wave * HS_RB;
         F kfr[4];
 #pragma unroll
@@ -330,6 +329,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
             sa = Mma16<T>::mma(qa[ks], kfr[ks], sa);
             dp = Mma16<T>::mma(oa[ks], as_frag<T>(vf[ks]), dp);
           }
+          // P = exp2(S c - L), dS = P dP; the causal compare runs on every tile (off the diagonal it is never
+          // true): specializing the diagonal tiles measured 1 % slower (profiles/r4_fa_bwd_hs.md)
 #pragma unroll
           for (int g4 = 0; g4 < 4; ++g4) {
             const float4 L4 = *reinterpret_cast<const float4*>(Ls + 32 * t + 16 * hh + 4 * g4);
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
             for (int u = 0; u < 4; ++u) {
               const int r = 4 * g4 + u;
               float pv = fexp2(fmaf(sa[r], c2, Lv[u]));
-              if (diag && kq > 32 * t + 8 * g4 + u) pv = 0.f;
+              if (CAUSAL && kq > 32 * t + 8 * g4 + u) pv = 0.f;
               sa[r] = pv;
               dp[r] = pv * dp[r];
             }
@@ -373,20 +374,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
           }
         }
       }
-      // the dQ store's RoPE coefficients (row qrow, pairs of d 32dqt + 8g4 + 4hh ..), loaded ahead of the
-      // barrier so their L2 latency runs under it and the dQ product
-      float2 rcs[4], rsn[4];
-      if (ROPE == 1 && last) {
-        const int64_t pos = bp.f.rope_pos ? bp.f.rope_pos[(int64_t)b * N + qrow] : qrow;
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int64_t o = pos * (HS_D / 2) + 16 * dqt + 4 * g4 + 2 * hh;
-          rcs[g4] = *reinterpret_cast<const float2*>(rope.cs + o);
-          rsn[g4] = *reinterpret_cast<const float2*>(rope.sn + o);
-        }
-      }
       dma_barrier();  // D: dSᵀ of every group written, every wave done with this slot
-
       // E: dQᵀ tile = Kᵀ dSᵀ over the active groups (+ the earlier blocks' partial sums)
       {
         const int ng = CAUSAL ? min(4, (q0 + HS_BQ - kbase) / 32) : 4;  // active groups: 0 .. ng-1
@@ -421,10 +409,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
             v2 *= sc;
             v3 *= sc;
             if constexpr (ROPE == 1) {  // R(pos)ᵀ on the pairs (d, d+1), (d+2, d+3)
-              const float2 c = rcs[g4], sn = rsn[g4];
-              const float a0 = c.x * v0 + sn.x * v1, a1 = -sn.x * v0 + c.x * v1;
-              const float b0 = c.y * v2 + sn.y * v3, b1 = -sn.y * v2 + c.y * v3;
-              v0 = a0; v1 = a1; v2 = b0; v3 = b1;
+              const int64_t pos = bp.f.rope_pos ? bp.f.rope_pos[(int64_t)b * N + qrow] : qrow;
+              rope_inv4(v0, v1, v2, v3, rope, pos, d);
             }
             store4<T>(dQp + (int64_t)qrow * bp.dq_sn + d, make_float4(v0, v1, v2, v3));
           } else {
@@ -465,9 +451,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
 template <typename T, bool C, int R>
 void launch_hs(const AttnBwdParams& bp, float* rowc, float* part, hipStream_t s) {
   const int BH = bp.f.B * bp.f.H, N = bp.f.Nq;
-  if (N <= HS_MAXN && hs_in_kernel_delta()) {
-    hipLaunchKernelGGL((fa_bwd_hs_kernel<T, C, R, true>), dim3((unsigned)BH), dim3(256), 0, s, bp, rowc, part);
-    return;
+  // (the in-store RoPE option keeps the prep kernel: with both it needs more than 256 registers)
+  if constexpr (R != 1) {
+    if (N <= HS_MAXN && hs_in_kernel_delta()) {
+      hipLaunchKernelGGL((fa_bwd_hs_kernel<T, C, R, true>), dim3((unsigned)BH), dim3(256), 0, s, bp, rowc, part);
+      return;
+    }
   }
   hipLaunchKernelGGL((fa_bwd_hs_prep<T>), dim3((unsigned)(BH * (N / HS_BQ))), dim3(256), 0, s, bp, rowc);
   hipLaunchKernelGGL((fa_bwd_hs_kernel<T, C, R, false>), dim3((unsigned)BH), dim3(256), 0, s, bp, rowc, part);
