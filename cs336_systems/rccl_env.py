@@ -17,8 +17,9 @@ remains is a cap on stream-K grids (``TENSILE_STREAMK_MAX_CUS``) for any hipBLAS
 runs in a multi-rank job (a shape outside the table takes hipBLASLt's default untimed): it keeps a
 reserve of CUs free of stream-K workgroups, where RCCL channel blocks (256 threads, 21 KB LDS, <= 128
 VGPRs: several per CU) can always become resident. It costs the bench nothing (no hipBLASLt GEMM runs
-in its step), and a kernel trace shows it does not bind on the projection shapes either: hipBLASLt
-sizes their stream-K grids to 224-240 workgroups by itself, with or without the cap
+in its step). Kernel traces show it does not bind on the projection shapes either: hipBLASLt sizes
+their stream-K grids to 224-240 workgroups by itself, and this image's hipBLASLt leaves them
+unchanged even at a cap of 128 -- the variable is inert here and kept for builds that honour it
 (``profiles/r4_streamk_cap.md``). The RCCL channel cap of round 3 (``NCCL_MAX_NCHANNELS=32``) is dropped: it only bought
 safety beside stream-K grids, which the step no longer has, and it capped the all-reduce bandwidth of
 every collective. ``scripts/coresidency_probe.py`` / ``tests/test_coresidency_gpu.py`` measure the
