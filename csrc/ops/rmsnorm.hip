@@ -320,9 +320,15 @@ template <int NV, typename F>
 void dispatch_nv(int H, F&& f) {
   (void)NV;
   const int per_lane = (H / 4 + kWave - 1) / kWave;
+  // 10 and 12 (d_model 2560 / 3072): rounding them up to 16 left the backward at one wave per SIMD
+  // (256 VGPRs + AGPRs) and 66 % of the HBM rate in the 2.7b step (profiles/r4_2p7b_roofline_b24.md)
   if (per_lane <= 2) f(std::integral_constant<int, 2>{});
   else if (per_lane <= 4) f(std::integral_constant<int, 4>{});
   else if (per_lane <= 8) f(std::integral_constant<int, 8>{});
+#ifndef CS336_RMS_NV16  // A/B probe: the round-3 rounding (10 and 12 -> 16)
+  else if (per_lane <= 10) f(std::integral_constant<int, 10>{});
+  else if (per_lane <= 12) f(std::integral_constant<int, 12>{});
+#endif
   else if (per_lane <= 16) f(std::integral_constant<int, 16>{});
   else f(std::integral_constant<int, 32>{});
 }

@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.mark.parametrize("H", [64, 1600, 2560])
+@pytest.mark.parametrize("H", [64, 1600, 2560, 3072])
 @pytest.mark.parametrize("xdt,rdt", [(torch.float32, torch.bfloat16), (torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16)])
 @pytest.mark.parametrize("with_ds", [True, False])
 def test_add_rmsnorm(H, xdt, rdt, with_ds):

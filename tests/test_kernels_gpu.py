@@ -22,7 +22,7 @@ def test_extension_loaded():
 
 
 # ---------------------------------------------------------------------------------- RMSNorm
-@pytest.mark.parametrize("H", [64, 1600, 2560, 4100])
+@pytest.mark.parametrize("H", [64, 1600, 2560, 3072, 4100])
 @pytest.mark.parametrize("xdt,odt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16), (torch.bfloat16, torch.bfloat16)])
 def test_rmsnorm(H, xdt, odt):
     torch.manual_seed(0)
