@@ -60,15 +60,6 @@ constexpr int HS_LDS_IND = HS_OFF_DH + HS_MAXN * 4;
 static_assert(HS_LDS_IND <= 80 * 1024, "two workgroups per CU");
 constexpr int HS_SLICE_DMA = 2 * (HS_BQ * (HS_RB / 16) / 256);  // Q + dO wave-instructions per wave
 
-// CS336_HS_PRIO (probe): raise the wave's issue priority around its MFMA clusters (guide T5), so
-// the partner wave's VALU does not delay them
-template <int P>
-__device__ __forceinline__ void hs_prio() {
-#ifdef CS336_HS_PRIO
-  __builtin_amdgcn_s_setprio(P);
-#endif
-}
-
 // CS336_FA_HS_DELTA=0: row constants from the prep kernel instead of the in-kernel delta
 inline bool hs_in_kernel_delta() {
   const char* e = getenv("CS336_FA_HS_DELTA");
@@ -333,13 +324,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
           }
           f32x16 dp = *reinterpret_cast<const f32x16*>(Ds + 32 * t + 16 * hh);
           f32x16 sa = zero16();
-          hs_prio<1>();
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks) {
             sa = Mma16<T>::mma(qa[ks], kfr[ks], sa);
             dp = Mma16<T>::mma(oa[ks], as_frag<T>(vf[ks]), dp);
           }
-          hs_prio<0>();
           // P = exp2(S c - L), dS = P dP; the causal compare runs on every tile (off the diagonal it is never
           // true): specializing the diagonal tiles measured 1 % slower (profiles/r4_fa_bwd_hs.md)
 #pragma unroll
@@ -369,13 +358,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
               ot[s2] = trf2(dOt + 16 * s2 * HS_RB, toa[dt], tob[dt]);
               qt[s2] = trf2(Qt + 16 * s2 * HS_RB, toa[dt], tob[dt]);
             }
-            hs_prio<1>();
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
               dv[dt] = Mma16<T>::mma(ot[s2], pf[s2], dv[dt]);
               dk[dt] = Mma16<T>::mma(qt[s2], sf[s2], dk[dt]);
             }
-            hs_prio<0>();
           }
           // dSᵀ row (block-local key 32 wave + l32): query halves 32t + 16s2 + 4hh + 0..3 and + 8
 #pragma unroll
