@@ -28,9 +28,10 @@ def main():
     lo, hi = starts[-2], starts[-1]
     step = [x for x in iv if lo <= x[0] < hi]
     fwd_fa = [i for i, x in enumerate(step) if "fa_fwd" in x[2]]
-    # one FA backward anchor per layer: the fused forms' first launch (the hs / kp prep kernel), or
-    # the dQ kernel of the two-kernel form
-    anchors = ("fa_bwd_dq", "fa_bwd_fused", "fa_bwd_hs_prep", "fa_bwd_kp_prep")
+    # one FA backward anchor per layer: the two-kernel form's dQ kernel, the fused kernel, the kp prep
+    # launch, or the hs main kernel (its prep launch, when CS336_FA_HS_DELTA=0, then ends the listing
+    # of the layer before)
+    anchors = ("fa_bwd_dq", "fa_bwd_fused", "fa_bwd_kp_prep", "fa_bwd_hs_kernel")
     bwd_fa = [i for i, x in enumerate(step) if any(a in x[2] for a in anchors)]
     L = a.layer
     print(f"== forward, layer {L}")
