@@ -107,10 +107,11 @@ def parse(argv=None):
     # vocabulary head, launch tails) amortize over twice the tokens, and under DDP the backward that
     # hides each step's 8 GB gradient all-reduce doubles. (Round 2, hipBLASLt-era sweep:
     # profiles/r2_batch_sweep.md.) The committed GEMM table and dW plans cover 24576 and 49152 tokens.
-    # (2.7b: 24 x 1024 = 24576 tokens per GPU by default, 136 GiB: at 12 x 1024 every d_model-wide
-    # GEMM output has only 384 tiles of 256 x 320 for 256 CUs; 51.2k vs 45.6k tok/s,
-    # profiles/r4_bench_2p7b.md)
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: xl 96, 2.7b 24576 tokens / ctx)")
+    # (2.7b: 32 x 1024 = 32768 tokens per GPU by default, 164 GiB: 53.2-53.4k tok/s vs 51.6k at 24 x 1024
+    # (136 GiB) and 45.6k at 12 x 1024, where every d_model-wide GEMM output has only 384 tiles of
+    # 256 x 320 for 256 CUs; profiles/r4_bench_2p7b.md, the committed table covers 12288, 24576 and
+    # 32768 tokens)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: xl 96, 2.7b 32768 tokens / ctx)")
     ap.add_argument("--vocab", type=int, default=10000)
     ap.add_argument(
         "--ddp",
@@ -182,7 +183,7 @@ def parse(argv=None):
     a = ap.parse_args(argv)
     if a.batch is None:
         env = os.environ.get("CS336_BENCH_BATCH")
-        a.batch = int(env) if env else (max(1, 24576 // a.ctx) if a.model == "2.7b" else 96)
+        a.batch = int(env) if env else (max(1, 32768 // a.ctx) if a.model == "2.7b" else 96)
     return a
 
 
