@@ -14,11 +14,14 @@
 // over a 128-key block and needs 66 KiB, so two independent workgroups share every CU: while one
 // waits on a barrier or a memory round trip, the other's MFMAs run on the same SIMDs.
 //
-// Layout per workgroup (66 KiB of LDS):
+// Layout per workgroup (78 KiB of LDS; two fit a CU's 160 KiB):
 //   2 slots x {Q slice image 8 KiB | dO slice image 8 KiB | row constants 1 KiB}   (LDS-DMA)
 //   K block image 16 KiB (LDS-DMA, once per key block) | dSᵀ image 16 KiB
-// Row constants (-lse·log2 e and -delta, delta = rowsum(dO·O), in the accumulator row order) come from
-// a small prep kernel (one pass over O and dO), as in fa_bwd_kp.hip.
+//   O slice image 8 KiB | -delta of the whole head 4 KiB (N <= 1024)
+// delta = rowsum(dO·O) is computed here during the first key block (every slice passes once), from
+// the dO image the item staged anyway and an O image staged one item ahead; the slot's row constants
+// are then the slice's raw lse. For N > 1024 (or CS336_FA_HS_DELTA=0) a prep kernel writes both row
+// constants instead (one pass over O and dO, as fa_bwd_kp.hip) and the kernel needs 66 KiB.
 //
 // Wave w owns keys 32w .. 32w+31 of the block (key on the MFMA lane), keeps their dKᵀ / dVᵀ (fp32)
 // and V (the B operand of dP) in registers, and per 64-query slice, one 32-query tile at a time:
