@@ -445,8 +445,11 @@ def main(argv=None):
     sync()
     timing["on"] = True
     t_start = time.perf_counter()
+    sync_each = os.environ.get("CS336_BENCH_SYNC_EACH", "0") == "1"  # diagnostic: no host run-ahead
     for i in range(args.steps):
         loss = step(i)
+        if sync_each:
+            sync()
     sync()
     barrier()
     elapsed = time.perf_counter() - t_start
@@ -462,6 +465,12 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     peak_gib = torch.cuda.max_memory_allocated(device) / 2**30 if device.type == "cuda" else 0.0
+    if device.type == "cuda":  # allocator churn inside the timed steps (cudaFree/cudaMalloc retries)
+        ms = torch.cuda.memory_stats(device)
+        log(
+            f"allocator: reserved peak {ms.get('reserved_bytes.all.peak', 0) / 2**30:.1f} GiB, "
+            f"alloc retries {ms.get('num_alloc_retries', 0)}, device mallocs {ms.get('num_device_alloc', 0)}"
+        )
 
     ms_per_step = 1e3 * elapsed / max(args.steps, 1)
     tokens_per_step = args.batch * args.ctx * world
