@@ -306,6 +306,23 @@ def compute_weight(params: list[nn.Parameter], dtype: torch.dtype) -> torch.Tens
 # hazard cs336_systems/rccl_env.py caps (profiles/r3_coresidency.md).
 _SIDE_STREAMS: dict[int, torch.cuda.Stream] = {}
 _state = {"dirty": False, "callback": False}
+# Inputs of in-flight side-stream dW GEMMs, oldest first: (event recorded after the GEMM, the
+# main-stream tensors it reads). They are held here instead of ``record_stream``-ed: a block
+# freed with a side-stream use cannot be reused until the allocator sees that use complete, and
+# with the host steps ahead of the GPU every layer's dY / X then needs a fresh block
+# (profiles/r4_dw_stream.md). Past _SIDE_LAG entries the main stream waits for the oldest GEMM
+# and the tensors are released in main-stream order.
+_SIDE_PENDING: list[tuple[torch.cuda.Event, tuple[torch.Tensor, ...]]] = []
+_SIDE_LAG = 2
+
+
+def _hold_for_side(main: torch.cuda.Stream, side: torch.cuda.Stream, *ts: torch.Tensor) -> None:
+    ev = torch.cuda.Event()
+    ev.record(side)
+    _SIDE_PENDING.append((ev, ts))
+    while len(_SIDE_PENDING) > _SIDE_LAG:
+        old, _ = _SIDE_PENDING.pop(0)
+        main.wait_event(old)
 
 
 def dw_stream_enabled() -> bool:
@@ -327,6 +344,7 @@ def sync_dw_stream() -> None:
     _state["dirty"] = False
     for idx, s in _SIDE_STREAMS.items():
         torch.cuda.current_stream(idx).wait_stream(s)
+    _SIDE_PENDING.clear()  # after the wait: their blocks are reused in main-stream order
 
 
 def dw_stream_for(t: torch.Tensor) -> torch.cuda.Stream | None:
@@ -568,8 +586,11 @@ class FusedLinearFn(torch.autograd.Function):
                 s.wait_stream(main)
                 with torch.cuda.stream(s):
                     dw = dw_fn(target, True)  # beside the main stream's GEMMs: no stream-K
-                dy2.record_stream(s)
-                x2.record_stream(s)
+                if os.environ.get("CS336_DW_HOLD", "1") == "1":
+                    _hold_for_side(main, s, dy2, x2)
+                else:  # the round-4 form, kept for the A/B (scripts/r4_dws_alloc.sh)
+                    dy2.record_stream(s)
+                    x2.record_stream(s)
                 if target is None:
                     dw.record_stream(main)
                 _mark_side_work()
