@@ -32,8 +32,9 @@ sys.path.insert(0, REPO)
 from cs336_systems.rccl_env import apply_multi_gpu_env  # noqa: E402  (torch-free)
 
 if __name__ == "__main__":
-    # stream-K grid cap + RCCL channel cap for multi-rank runs, set before torch loads hipBLASLt/RCCL
-    # (cs336_systems/rccl_env.py, profiles/r3_coresidency.md)
+    # stream-K grid cap for multi-rank runs (the RCCL channel cap was dropped in round 4; the cap is
+    # inert on this image and kept for hipBLASLt builds that honour it), set before torch loads
+    # hipBLASLt/RCCL (cs336_systems/rccl_env.py, profiles/r4_streamk_cap.md)
     _CORES_ENV = apply_multi_gpu_env(int(os.environ.get("WORLD_SIZE", "1")))
 else:
     _CORES_ENV = {}
@@ -81,7 +82,8 @@ class SweepWatchdog:
             if self._done:
                 return
             self._done = True
-        self.out.setdefault("dist", {})["ddp_sweep"] = {"error": f"timed out after {self.limit_s:g} s"}
+        self.out.setdefault("dist", {})["ddp_sweep"] = {"error": f"timed out after {self.limit_s:g} s",
+                                                        "watchdog": True}
         if self.rank == 0:
             log(f"DDP sweep exceeded {self.limit_s:g} s: reporting the headline result without it")
             emit_result(self.out, self.json_out)

@@ -240,19 +240,43 @@ def sweep_variants(model_name: str, ctx: int, per_rank_batch: int, dev: torch.de
         if rank == 0:
             print(f"ddp sweep: {msg} ({time.perf_counter() - t_start:.1f} s)", file=__import__("sys").stderr, flush=True)
 
+    def failed_anywhere(local_error: bool) -> bool:
+        """Every rank learns whether any rank's variant raised. A rank that raised (an OOM inside
+        run(), say) left its peers inside collectives of that variant; continuing on the failing rank
+        alone would pair its next collectives with theirs. So after a failure anywhere the
+        whole sweep stops, together, on every rank."""
+        f = torch.tensor([1.0 if local_error else 0.0], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
+        return f.item() > 0
+
+    aborted = False
     for variant, bucket_mb in variants:
         row = {"variant": variant, "bucket_mb": bucket_mb}
         note(f"{variant} {bucket_mb if bucket_mb is not None else ''}")
-        if over_budget():
+        if aborted:
+            row["skipped"] = "an earlier variant failed on some rank"
+        elif over_budget():
             row["skipped"] = "time budget"
         else:
+            err = None
             try:
                 st, cw, *_ = run(variant, bucket_mb)
                 row.update(ms_per_step=round(st, 3), comm_wait_ms=round(cw, 3),
                            comm_fraction=round(cw / st, 4) if st else 0.0)
             except Exception as e:  # noqa: BLE001 - reported in the JSON, never loses the headline
-                row["error"] = f"{type(e).__name__}: {e}"[:300]
+                err = row["error"] = f"{type(e).__name__}: {e}"[:300]
+            # every rank exchanges the flag, the failing one included: an error raised at a variant
+            # boundary (model build, OOM before the first bucket) stops the sweep on all ranks
+            # together; one raised inside a collective sequence leaves the peers in that sequence,
+            # where bench.py's SweepWatchdog bounds the wait and marks the sweep timed out
+            if failed_anywhere(err is not None):
+                aborted = True
+                row.setdefault("error", "failed on another rank")
         rows.append(row)
+    if aborted:
+        zero1 = False
+        mem = {"skipped": "an earlier variant failed on some rank"}
     if zero1:
         if over_budget():
             mem = {"skipped": "time budget"}

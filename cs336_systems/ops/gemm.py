@@ -139,7 +139,10 @@ def _pick(kind: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None,
         # here, on a cache miss, not on every call
         if any(hasattr(fn, "partial_bytes") for fn in cands.values()):
             free = torch.cuda.mem_get_info()[0]
-            cands = {n: fn for n, fn in cands.items() if getattr(fn, "partial_bytes", 0) + (4 << 30) <= free}
+            # only the split-K candidates are filtered: "blas" (and any candidate without partials)
+            # always stays, so the comparison below never runs on an empty or blas-less set
+            cands = {n: fn for n, fn in cands.items()
+                     if not hasattr(fn, "partial_bytes") or fn.partial_bytes + (4 << 30) <= free}
         times = {name: _time_ms(fn) for name, fn in cands.items()}
         best = min(times, key=times.get)
         hit = _BEST[key] = best if times[best] < 0.97 * times["blas"] else "blas"

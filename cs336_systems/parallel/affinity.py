@@ -68,8 +68,24 @@ def gpu_local_cpus(device_index: int, sysfs: str = "/sys/bus/pci/devices") -> tu
         return None, addr
 
 
+def _pin_all_threads(cpus: list[int]) -> tuple[int, int]:
+    """Set ``cpus`` as the affinity of every thread in /proc/self/task; (threads set, threads seen)."""
+    try:
+        tids = [int(t) for t in os.listdir("/proc/self/task")]
+    except OSError:
+        return 0, 0
+    ok = 0
+    for tid in tids:
+        try:
+            os.sched_setaffinity(tid, cpus)
+            ok += 1
+        except OSError:  # the thread exited meanwhile, or is not ours to move
+            pass
+    return ok, len(tids)
+
+
 def pin_rank_to_gpu(device) -> dict:
-    """Pin this process to the CPUs local to ``device`` (a CUDA/HIP device); returns what happened
+    """Pin this process (every thread of it) to the CPUs local to ``device`` (a CUDA/HIP device); returns what happened
     (also kept for :func:`affinity_info`). CPU devices and unknown topologies leave the mask as is."""
     info: dict = {"pinned": False}
     try:
@@ -89,6 +105,11 @@ def pin_rank_to_gpu(device) -> dict:
                     info["pinned"] = True
                 except OSError as e:
                     info["error"] = str(e)
+                # sched_setaffinity(0) pins only the calling thread: the HIP runtime's threads (and an
+                # OpenMP pool) started before this call keep the full mask, so apply it to every
+                # thread of the process and report how many took it
+                n_ok, n_all = _pin_all_threads(want)
+                info["threads_pinned"] = f"{n_ok}/{n_all}"
             elif want:
                 info["pinned"] = True  # already exactly the local set
     try:

@@ -46,8 +46,9 @@ import time
 
 from .rccl_env import apply_multi_gpu_env
 
-# co-residency caps for multi-rank runs (stream-K grid cap, RCCL channel cap), set before torch loads
-# hipBLASLt / RCCL, exactly as bench.py does
+# multi-rank environment (the hipBLASLt stream-K grid cap, kept for hipBLASLt builds that honour it:
+# profiles/r4_streamk_cap.md measured it inert on this image), set before torch loads hipBLASLt,
+# exactly as bench.py does
 _CORES_ENV = apply_multi_gpu_env(int(os.environ.get("WORLD_SIZE", "1")))
 
 import numpy as np  # noqa: E402

@@ -985,6 +985,11 @@ void gemm8(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, int64_t epi,
   TORCH_CHECK(cs336::gemm8::launch(p, (int)epi, (int)fn, stream()), "cs336: gemm8 launch (fn ", fn, ")");
 }
 
+// first-round workgroup stagger of gemm8 per epilogue (csrc/gemm/gemm8.hip, set_stagger)
+bool gemm8_stagger(int64_t epi, int64_t ticks, int64_t groups) {
+  return cs336::gemm8::set_stagger((int)epi, (int)ticks, (int)groups);
+}
+
 // QKV projection forward with RoPE in the store (gemm8 epi 3): c = a @ b.T with columns < rope_cols
 // rotated (interleaved pairs, d_head dhead) at position pos[row] (pos: int64 per row, or None: row % seq).
 void gemm8_rope(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, const at::Tensor& cos, const at::Tensor& sin,
@@ -1136,6 +1141,7 @@ TORCH_LIBRARY(cs336, m) {
   m.def("cohort(int n_workgroups, int lds_bytes, float deadline_ms, Tensor(a!) state) -> ()");
   m.def("gemm8(Tensor a, Tensor b, Tensor(a!) c, int epi, int fn, Tensor(b!)? h, Tensor? y, int half) -> ()");
   m.def("gemm8_ok(int M, int N, int K, int epi, int half) -> bool", &gemm8_ok);
+  m.def("gemm8_stagger(int epi, int ticks, int groups) -> bool", &gemm8_stagger);
   m.def("gemm8_rope(Tensor a, Tensor b, Tensor(a!) c, Tensor cos, Tensor sin, Tensor? pos, int seq, int rope_cols, int dhead) -> ()");
   m.def("gemm8w(Tensor a, Tensor b, Tensor(a!) out, int splits, bool trans_out, bool accumulate, int fn) -> ()");
   m.def("multi_tensor_scale_(Tensor(a!)[] tensors, Tensor scale) -> ()");

@@ -47,6 +47,7 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int v4u32;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 constexpr int BM = 256, BK = 64, NT = 512;
@@ -100,11 +101,26 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   constexpr bool NTAIL = TAIL & 1, KTAIL = TAIL & 2;
   using G = Geo<FN>;
   constexpr int BN = G::BN, WTN = G::WTN, FB0 = G::FB0, B0C = G::B0C, STAGE = G::STAGE;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  // the main loop's two stages, or (epilogue) the whole bf16 tile image
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE > BM * BN * 2 ? 2 * STAGE : BM * BN * 2];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
+
+  // ---- first-round stagger -------------------------------------------------------------------
+  // One workgroup per CU and equal tiles keep every CU in lockstep: all reach the epilogue together
+  // and its HBM traffic (EPI 1/2: 0.25-0.65 MB per tile) runs as one chip-wide burst while no CU
+  // multiplies. Delaying groups of first-round workgroups (later ones inherit the offset: a CU takes
+  // its next tile when it frees) spreads the bursts over other CUs' main loops.
+  if (p.stg_ticks > 0 && (int)blockIdx.x < p.stg_first) {
+    const int g = (int)(blockIdx.x >> 3) % p.stg_groups;
+    if (g) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      const uint64_t wait = (uint64_t)g * (uint64_t)p.stg_ticks;
+      while (__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(2);
+    }
+  }
 
   // ---- tile coordinates -------------------------------------------------------------------
   // EPI 1: N = 2·half, BN/2 units of each half per tile. EPI 0 also takes an N tail (N % BN != 0,
@@ -315,109 +331,157 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   sbarrier();
 
   // ---- epilogue ----------------------------------------------------------------------------
-  // Lane l holds C[m = l&15][n = 4(l>>4) + r] of each 16x16 block (operand-swapped MFMA). Blocks go
-  // through a per-wave LDS scratch [rows][WTN] (8-B bf16 / 16-B fp32 writes), then leave as whole
-  // 16-B row pieces (8 columns) per lane, fully unrolled.
-  constexpr int CPR = WTN / 8;  // 8-column units per scratch row
+  // cache policy of the epilogue's streams: the SwiGLU outputs (EPI 1 y and h, EPI 2 da|db) and the
+  // EPI 2 a/b inputs are touched once here, so they go out / come in nontemporal (aux bit 1 = nt):
+  // -7 % on W1|W3 forward and -6 % on the W2 input gradient from nt stores, a further -7 % on the
+  // latter from nt a/b loads (49152 tokens, same box; profiles/r5_gemm8_epilogue.md). Plain EPI 0
+  // stores stay default-policy (their consumer usually reads them next; nt measured neutral there)
+  constexpr int ST_AUX = EPI == 0 ? 0 : 2, LD_AUX = 2;
+  // Lane l holds C[m = l&15][n = 4(l>>4) + r] of each 16x16 block (operand-swapped MFMA).
   const int m_l = lane & 15, n_l = 4 * (lane >> 4);
-  if constexpr (EPI == 2) {
-    // dh (fp32) in 32-row pieces: scratch 32 × WTN × 4 B per wave (≤ 80 KiB in all)
-    constexpr int PR = 32, UNITS = PR * CPR, PER = UNITS / 64;
-    static_assert(UNITS % 64 == 0, "epilogue units must fill the wave");
-    char* scr = smem + wave * (PR * WTN * 4);
-    constexpr int NP = 8 / (PR / 16);  // pieces
-    // a/b loads software-pipelined one piece ahead (two register buffers): a piece's loads are in
-    // flight while the previous piece is computed and stored, so the tile pays about one load
-    // latency instead of one per piece
-    uint4 av[2][PER], bv[2][PER];
-    auto load_ab = [&](int piece, uint4 (&ab)[PER], uint4 (&bb)[PER]) {
-#pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int q = lane + 64 * u, rr = q / CPR, cc = q % CPR;
-        const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
-        const int col = n0 + bcol + cc * 8;
-        ab[u] = *reinterpret_cast<const uint4*>(p.y + row * p.ldy + col);
-        bb[u] = *reinterpret_cast<const uint4*>(p.y + row * p.ldy + p.half + col);
-      }
+  if constexpr (EPI != 3) {
+    // Whole-tile epilogue (EPI 0/1/2): every wave dumps its blocks as bf16 into one [256][BN] image
+    // that fills the LDS (160 KiB at BN 320), then the workgroup streams it out row-major: each
+    // wave instruction covers whole 640-B (320-B) row runs instead of the 160-B pieces of a per-wave
+    // scratch. EPI 2 issues ALL of the thread's a/b loads (20 + 20 x 16 B) as soon as the
+    // accumulators are dumped: the round-3/4 form kept one 32-row piece in flight and was
+    // latency-bound (ablation: the a/b loads were 0.22 of 1.14 ms, profiles/r5_gemm8_epilogue.md).
+    // EPI 2 rounds dh to bf16 before the SwiGLU backward, as the unfused path (bf16 GEMM output) does.
+    // Image chunks (16 B = 8 columns) are XOR-swizzled by the row: conflict-free 8-B dump writes
+    // (16 rows per lane group) and 16-B row-major reads.
+    constexpr int RB = BN * 2, CH = BN / 8;
+    auto img = [&](int row, int ch) -> uint32_t {
+      const int x = FN == 5 ? ((row >> 1) & 7) : (row & 15);
+      return (uint32_t)(row * RB + ((ch ^ x) << 4));
     };
-    load_ab(0, av[0], bv[0]);
 #pragma unroll
-    for (int piece = 0; piece < NP; ++piece) {
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int ib = 0; ib < PR / 16; ++ib)
+      for (int j = 0; j < FN; ++j) {
+        const f32x4 v = acc[i][j];
+        const int row = arow + 16 * i + m_l, col = bcol + 16 * j + n_l;
+        const uint32_t lo = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+        const uint32_t hi = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+        *reinterpret_cast<uint2*>(smem + img(row, col >> 3) + ((col >> 2) & 1) * 8) = make_uint2(lo, hi);
+      }
+    // output (and EPI 2 input) descriptors based at the tile's first row; 32-bit offsets within it
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.c + (int64_t)m0 * p.ldc), (short)0, 0x7fffffffu, 0x00020000);
+    if constexpr (EPI == 2) {
+      constexpr int PT = BM * CH / NT;  // 20 (BN 320) or 16 chunks per thread
+      static_assert(BM * CH % NT == 0, "chunks must split over the workgroup");
+      const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(p.y + (int64_t)m0 * p.ldy), (short)0, 0x7fffffffu, 0x00020000);
+      uint4 av[PT], bv[PT];
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const f32x4 v = acc[piece * (PR / 16) + ib][j];
-          *reinterpret_cast<f32x4*>(scr + ((16 * ib + m_l) * WTN + 16 * j + n_l) * 4) = v;
-        }
-      __builtin_amdgcn_wave_barrier();
-      if (piece + 1 < NP) load_ab(piece + 1, av[(piece + 1) & 1], bv[(piece + 1) & 1]);
+      for (int i = 0; i < PT; ++i) {
+        const int q = tid + NT * i, row = q / CH, ch = q % CH;
+        const uint32_t off = 2u * (uint32_t)(row * p.ldy + n0 + 8 * ch);
+        av[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, LD_AUX));
+        bv[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ry, off + 2u * (uint32_t)p.half, 0, LD_AUX));
+      }
+      lgkm0();
+      sbarrier();  // image complete
 #pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int q = lane + 64 * u, rr = q / CPR, cc = q % CPR;
-        const float4 d0 = *reinterpret_cast<const float4*>(scr + (rr * WTN + cc * 8) * 4);
-        const float4 d1 = *reinterpret_cast<const float4*>(scr + (rr * WTN + cc * 8 + 4) * 4);
-        const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
-        const int col = n0 + bcol + cc * 8;
-        const float dh[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-        const bf16_t* ae = reinterpret_cast<const bf16_t*>(&av[piece & 1][u]);
-        const bf16_t* be = reinterpret_cast<const bf16_t*>(&bv[piece & 1][u]);
+      for (int i = 0; i < PT; ++i) {
+        const int q = tid + NT * i, row = q / CH, ch = q % CH;
+        const uint4 dv = *reinterpret_cast<const uint4*>(smem + img(row, ch));
+        const bf16_t* de = reinterpret_cast<const bf16_t*>(&dv);
+        const bf16_t* ae = reinterpret_cast<const bf16_t*>(&av[i]);
+        const bf16_t* be = reinterpret_cast<const bf16_t*>(&bv[i]);
         uint4 dav, dbv;
         bf16_t* da = reinterpret_cast<bf16_t*>(&dav);
         bf16_t* db = reinterpret_cast<bf16_t*>(&dbv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float a = bf16_to_f32(ae[e]), b = bf16_to_f32(be[e]);
-          const float sg = sigmoid_f(a), gb = dh[e] * sg;
+          const float a = bf16_to_f32(ae[e]), b = bf16_to_f32(be[e]), dh = bf16_to_f32(de[e]);
+          const float sg = sigmoid_f(a), gb = dh * sg;
           da[e] = f32_to_bf16(gb * b * (1.f + a * (1.f - sg)));
           db[e] = f32_to_bf16(gb * a);
         }
-        *reinterpret_cast<uint4*>(p.c + row * p.ldc + col) = dav;
-        *reinterpret_cast<uint4*>(p.c + row * p.ldc + p.half + col) = dbv;
+        const uint32_t off = 2u * (uint32_t)(row * p.ldc + n0 + 8 * ch);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, dav), rc, off, 0, ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, dbv), rc, off + 2u * (uint32_t)p.half, 0, ST_AUX);
       }
-      __builtin_amdgcn_wave_barrier();
-      lgkm0();  // this piece's scratch reads retired before the next piece's writes
+    } else if constexpr (EPI == 1) {
+      // tile columns [0, BN/2) are a = W1 units n0.., [BN/2, BN) b = W3 units: one thread takes a
+      // unit chunk pair, stores both halves of y and h = silu(a)·b
+      constexpr int HU = CH / 2, PT = BM * HU / NT;  // 10 (BN 320) or 8 pairs per thread
+      static_assert(BM * HU % NT == 0, "pairs must split over the workgroup");
+      const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(p.h + (int64_t)m0 * p.ldh), (short)0, 0x7fffffffu, 0x00020000);
+      lgkm0();
+      sbarrier();  // image complete
+#pragma unroll
+      for (int i = 0; i < PT; ++i) {
+        const int q = tid + NT * i, row = q / HU, u = q % HU;
+        const uint4 va = *reinterpret_cast<const uint4*>(smem + img(row, u));
+        const uint4 vb = *reinterpret_cast<const uint4*>(smem + img(row, u + HU));
+        const uint32_t off = 2u * (uint32_t)(row * p.ldc + n0 + 8 * u);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, va), rc, off, 0, ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, vb), rc, off + 2u * (uint32_t)p.half, 0, ST_AUX);
+        const bf16_t* ae = reinterpret_cast<const bf16_t*>(&va);
+        const bf16_t* be = reinterpret_cast<const bf16_t*>(&vb);
+        uint4 hv;
+        bf16_t* he = reinterpret_cast<bf16_t*>(&hv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float a = bf16_to_f32(ae[e]);
+          he[e] = f32_to_bf16(a * sigmoid_f(a) * bf16_to_f32(be[e]));
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, hv), rh, 2u * (uint32_t)(row * p.ldh + n0 + 8 * u), 0, ST_AUX);
+      }
+    } else {
+      constexpr int PT = BM * CH / NT;
+      lgkm0();
+      sbarrier();  // image complete
+#pragma unroll
+      for (int i = 0; i < PT; ++i) {
+        const int q = tid + NT * i, row = q / CH, ch = q % CH;
+        const uint4 v = *reinterpret_cast<const uint4*>(smem + img(row, ch));
+        const int col = n0 + 8 * ch;
+        if (!NTAIL || col < p.N)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rc, 2u * (uint32_t)(row * p.ldc + col), 0, ST_AUX);
+      }
     }
   } else {
-    // bf16 in 64-row pieces: scratch 64 × WTN × 2 B per wave (≤ 80 KiB in all); EPI 3: 32-row
-    // pieces (40 KiB), and the tile rows' RoPE cos/sin staged in the LDS behind them, so the store
-    // loop reads no global memory (a global load there waits for every earlier store: vmcnt retires
-    // in issue order)
-    constexpr int PR = EPI == 3 ? 32 : 64, UNITS = PR * CPR, PER = UNITS / 64;
+    // EPI 3 (QKV + RoPE): per-wave scratch in 32-row pieces (40 KiB in all), the tile rows' RoPE
+    // cos/sin staged in the LDS behind it, so the store loop reads no global memory (a global load
+    // there waits for every earlier store: vmcnt retires in issue order)
+    constexpr int CPR = WTN / 8;  // 8-column units per scratch row
+    constexpr int PR = 32, UNITS = PR * CPR, PER = UNITS / 64;
     static_assert(UNITS % 64 == 0, "epilogue units must fill the wave");
     char* scr = smem + wave * (PR * WTN * 2);
-    constexpr int TOFF = 8 * PR * WTN * 2;  // EPI 3 table: cos [256][np], then sin [256][np] (fp32)
-    const int np = EPI == 3 ? (p.rdh >> 1) : 0;
-    const bool rot = EPI == 3 && n0 < p.rope_cols;  // tile-uniform (host: rope_cols % BN == 0)
-    if constexpr (EPI == 3) {
-      static_assert(TOFF + 2 * 256 * 48 * 4 <= 2 * STAGE, "cos/sin table of d_head <= 96 behind the scratch");
-      if (rot) {
-        // two threads per tile row, each half of the row's np/4 float4 of cos and of sin: every load
-        // issued before any is waited for (d_head <= 96: at most 6 float4 per thread and table)
-        constexpr int MAXQ = 6;
-        float* tc = reinterpret_cast<float*>(smem + TOFF);
-        float* ts = tc + 256 * np;
-        const int r = tid >> 1, q4n = np >> 2, hq = (q4n + 1) >> 1;
-        const int qb = (tid & 1) * hq;
-        const int row = m0 + r;
-        const int64_t pos = p.rpos ? p.rpos[row] : (int64_t)(row % p.rseq);
-        // indices past this thread's share are clamped to the row's last float4: a duplicate load
-        // and an identical rewrite, never a branch (keeps the arrays in registers)
-        float4 cb[MAXQ], sb[MAXQ];
+    constexpr int TOFF = 8 * PR * WTN * 2;  // table: cos [256][np], then sin [256][np] (fp32)
+    const int np = p.rdh >> 1;
+    const bool rot = n0 < p.rope_cols;  // tile-uniform (host: rope_cols % BN == 0)
+    static_assert(TOFF + 2 * 256 * 48 * 4 <= 2 * STAGE, "cos/sin table of d_head <= 96 behind the scratch");
+    if (rot) {
+      // two threads per tile row, each half of the row's np/4 float4 of cos and of sin: every load
+      // issued before any is waited for (d_head <= 96: at most 6 float4 per thread and table)
+      constexpr int MAXQ = 6;
+      float* tc = reinterpret_cast<float*>(smem + TOFF);
+      float* ts = tc + 256 * np;
+      const int r = tid >> 1, q4n = np >> 2, hq = (q4n + 1) >> 1;
+      const int qb = (tid & 1) * hq;
+      const int row = m0 + r;
+      const int64_t pos = p.rpos ? p.rpos[row] : (int64_t)(row % p.rseq);
+      // indices past this thread's share are clamped to the row's last float4: a duplicate load
+      // and an identical rewrite, never a branch (keeps the arrays in registers)
+      float4 cb[MAXQ], sb[MAXQ];
 #pragma unroll
-        for (int q = 0; q < MAXQ; ++q) {
-          const int i4 = min(qb + q, q4n - 1);
-          cb[q] = *reinterpret_cast<const float4*>(p.rcos + pos * np + 4 * i4);
-          sb[q] = *reinterpret_cast<const float4*>(p.rsin + pos * np + 4 * i4);
-        }
-#pragma unroll
-        for (int q = 0; q < MAXQ; ++q) {
-          const int i4 = min(qb + q, q4n - 1);
-          *reinterpret_cast<float4*>(tc + r * np + 4 * i4) = cb[q];
-          *reinterpret_cast<float4*>(ts + r * np + 4 * i4) = sb[q];
-        }
-        __syncthreads();
+      for (int q = 0; q < MAXQ; ++q) {
+        const int i4 = min(qb + q, q4n - 1);
+        cb[q] = *reinterpret_cast<const float4*>(p.rcos + pos * np + 4 * i4);
+        sb[q] = *reinterpret_cast<const float4*>(p.rsin + pos * np + 4 * i4);
       }
+#pragma unroll
+      for (int q = 0; q < MAXQ; ++q) {
+        const int i4 = min(qb + q, q4n - 1);
+        *reinterpret_cast<float4*>(tc + r * np + 4 * i4) = cb[q];
+        *reinterpret_cast<float4*>(ts + r * np + 4 * i4) = sb[q];
+      }
+      __syncthreads();
     }
 #pragma unroll
     for (int piece = 0; piece < 128 / PR; ++piece) {
@@ -430,83 +494,60 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
           const uint32_t hi = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
           *reinterpret_cast<uint2*>(scr + ((16 * ib + m_l) * WTN + 16 * j + n_l) * 2) = make_uint2(lo, hi);
         }
-      if constexpr (EPI == 1) {
-        lgkm0();
-        sbarrier();  // the partner wave (wc + 2: the same hidden units' b) wrote its piece
-      } else {
-        __builtin_amdgcn_wave_barrier();
-      }
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
         const int q = lane + 64 * u, rr = q / CPR, cc = q % CPR;
         const uint4 v = *reinterpret_cast<const uint4*>(scr + (rr * WTN + cc * 8) * 2);
         const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
-        if constexpr (EPI == 0) {
-          const int col = n0 + bcol + cc * 8;
-          if (!NTAIL || n0 + BN <= p.N || col < p.N) *reinterpret_cast<uint4*>(p.c + row * p.ldc + col) = v;
-        } else if constexpr (EPI == 3) {
-          const int col = n0 + bcol + cc * 8;
-          uint4 o = v;
-          if (rot) {  // q|k: rotate pairs (2i, 2i+1), i = (col mod d_head) / 2 + 0..3
-            const int i0 = (col % p.rdh) >> 1, tr = arow + PR * piece + rr;
-            const float* tc = reinterpret_cast<const float*>(smem + TOFF);
-            const float4 c4 = *reinterpret_cast<const float4*>(tc + tr * np + i0);
-            const float4 s4 = *reinterpret_cast<const float4*>(tc + 256 * np + tr * np + i0);
-            const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, sv[4] = {s4.x, s4.y, s4.z, s4.w};
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            uint32_t r[4];
+        const int col = n0 + bcol + cc * 8;
+        uint4 o = v;
+        if (rot) {  // q|k: rotate pairs (2i, 2i+1), i = (col mod d_head) / 2 + 0..3
+          const int i0 = (col % p.rdh) >> 1, tr = arow + PR * piece + rr;
+          const float* tc = reinterpret_cast<const float*>(smem + TOFF);
+          const float4 c4 = *reinterpret_cast<const float4*>(tc + tr * np + i0);
+          const float4 s4 = *reinterpret_cast<const float4*>(tc + 256 * np + tr * np + i0);
+          const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, sv[4] = {s4.x, s4.y, s4.z, s4.w};
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          uint32_t r[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float x0 = bf16_to_f32((bf16_t)(w[e] & 0xffff)), x1 = bf16_to_f32((bf16_t)(w[e] >> 16));
-              r[e] = (uint32_t)f32_to_bf16(cv[e] * x0 - sv[e] * x1) |
-                     ((uint32_t)f32_to_bf16(sv[e] * x0 + cv[e] * x1) << 16);
-            }
-            o = make_uint4(r[0], r[1], r[2], r[3]);
+          for (int e = 0; e < 4; ++e) {
+            const float x0 = bf16_to_f32((bf16_t)(w[e] & 0xffff)), x1 = bf16_to_f32((bf16_t)(w[e] >> 16));
+            r[e] = (uint32_t)f32_to_bf16(cv[e] * x0 - sv[e] * x1) |
+                   ((uint32_t)f32_to_bf16(sv[e] * x0 + cv[e] * x1) << 16);
           }
-          *reinterpret_cast<uint4*>(p.c + row * p.ldc + col) = o;
-        } else {
-          // tile col tc: a side (wc < 2) -> y[:, n0 + tc], b side -> y[:, half + n0 + tc - BN/2]
-          const int tc = bcol + cc * 8;
-          const int ycol = tc < BN / 2 ? n0 + tc : p.half + n0 + (tc - BN / 2);
-          *reinterpret_cast<uint4*>(p.c + row * p.ldc + ycol) = v;
+          o = make_uint4(r[0], r[1], r[2], r[3]);
         }
-      }
-      if constexpr (EPI == 1) {
-        // h = silu(a)·b for this piece, split between the two waves of a pair: the a-side wave
-        // (wc < 2) takes rows 0-31, its b-side partner (wc + 2) rows 32-63
-        constexpr int HU = (PR / 2) * CPR / 64;
-        static_assert(((PR / 2) * CPR) % 64 == 0, "h units must fill the wave");
-        const char* sa = smem + (wc < 2 ? wave : wave - 2) * (PR * WTN * 2);
-        const char* sb = smem + (wc < 2 ? wave + 2 : wave) * (PR * WTN * 2);
-        const int rbase = wc < 2 ? 0 : PR / 2;
-        const int acol0 = (wc & 1) * WTN;  // the pair's a columns within the tile's a half
-#pragma unroll
-        for (int u = 0; u < HU; ++u) {
-          const int q = lane + 64 * u, rr = rbase + q / CPR, cc = q % CPR;
-          const uint4 va = *reinterpret_cast<const uint4*>(sa + (rr * WTN + cc * 8) * 2);
-          const uint4 vb = *reinterpret_cast<const uint4*>(sb + (rr * WTN + cc * 8) * 2);
-          const bf16_t* ae = reinterpret_cast<const bf16_t*>(&va);
-          const bf16_t* be = reinterpret_cast<const bf16_t*>(&vb);
-          uint4 hv;
-          bf16_t* he = reinterpret_cast<bf16_t*>(&hv);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float a = bf16_to_f32(ae[e]);
-            he[e] = f32_to_bf16(a * sigmoid_f(a) * bf16_to_f32(be[e]));
-          }
-          const int64_t row = (int64_t)m0 + arow + PR * piece + rr;
-          *reinterpret_cast<uint4*>(p.h + row * p.ldh + n0 + acol0 + cc * 8) = hv;
-        }
+        *reinterpret_cast<uint4*>(p.c + row * p.ldc + col) = o;
       }
       lgkm0();
-      if constexpr (EPI == 1) sbarrier();  // partner reads done before the next piece overwrites
-      else __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_wave_barrier();
     }
   }
 }
 
+// per-epilogue first-round stagger: {ticks, groups}
+struct Stagger {
+  int ticks, groups;
+};
+Stagger g_stagger[4] = {{0, 1}, {0, 1}, {0, 1}, {0, 1}};
+
+int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 template <int FN, int EPI>
-void launch_t(const Args& p, hipStream_t s) {
+void launch_t(const Args& p_in, hipStream_t s) {
+  Args p = p_in;
+  p.stg_ticks = g_stagger[EPI].ticks;
+  p.stg_groups = g_stagger[EPI].groups;
+  p.stg_first = cu_count();
   constexpr int BN = 64 * FN;
   const int tail = EPI == 0 ? (p.N % BN != 0 ? 1 : 0) | (p.K % BK != 0 ? 2 : 0) : 0;
   const int tiles_n = (tail & 1) ? (p.N + BN - 1) / BN : p.N / BN;
@@ -529,6 +570,12 @@ void launch_t(const Args& p, hipStream_t s) {
 }
 
 }  // namespace
+
+bool set_stagger(int epi, int ticks, int groups) {
+  if (epi < 0 || epi > 3 || ticks < 0 || ticks > 100000 || groups < 1 || groups > 8) return false;
+  g_stagger[epi] = {groups > 1 ? ticks : 0, groups};
+  return true;
+}
 
 // Tile width for an output of N columns (EPI 1: N = 2·half): 320 if it divides, else 256, else 0.
 int pick_fn(int N, int epi, int half) {

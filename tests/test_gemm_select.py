@@ -1,0 +1,59 @@
+"""CPU test of the ``best``-mode GEMM selection (cs336_systems/ops/gemm.py ``_pick``): a low free-memory
+reading drops only the split-K candidates (those that carry ``partial_bytes``); "blas" always stays in
+the comparison (the filter used to drop every candidate under 4 GiB free)."""
+
+import torch
+
+from cs336_systems.ops import gemm
+
+
+def _cands():
+    def blas():
+        return None
+
+    def lt():
+        return None
+
+    def splitk():
+        return None
+
+    splitk.partial_bytes = 1 << 30
+    return {"blas": blas, "lt": lt, "cs336_sk": splitk}
+
+
+def _run(monkeypatch, free_bytes, times):
+    monkeypatch.setattr(gemm, "_BEST", {})
+    monkeypatch.setattr(gemm, "_BEST_TIMES", {})
+    monkeypatch.setattr(gemm, "selection_table", lambda: {})
+    monkeypatch.setattr(gemm, "_multi_rank", lambda: False)
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda *a, **k: (free_bytes, 288 << 30))
+    timed = []
+
+    def fake_time(fn, reps=5):
+        name = next(n for n, f in cands.items() if f is fn)
+        timed.append(name)
+        return times[name]
+
+    monkeypatch.setattr(gemm, "_time_ms", fake_time)
+    cands = _cands()
+    a, b = torch.empty(256, 64), torch.empty(64, 64)
+    pick = gemm._pick("fwd", a, b, None, cands)
+    return pick, timed
+
+
+def test_low_free_memory_keeps_blas(monkeypatch):
+    pick, timed = _run(monkeypatch, 1 << 30, {"blas": 1.0, "lt": 0.5, "cs336_sk": 0.1})
+    assert "blas" in timed and "lt" in timed and "cs336_sk" not in timed
+    assert pick == "lt"
+
+
+def test_ample_free_memory_times_split_k(monkeypatch):
+    pick, timed = _run(monkeypatch, 64 << 30, {"blas": 1.0, "lt": 0.5, "cs336_sk": 0.1})
+    assert set(timed) == {"blas", "lt", "cs336_sk"}
+    assert pick == "cs336_sk"
+
+
+def test_near_tie_prefers_blas(monkeypatch):
+    pick, _ = _run(monkeypatch, 1 << 30, {"blas": 1.0, "lt": 0.99, "cs336_sk": 0.1})
+    assert pick == "blas"
