@@ -20,6 +20,7 @@ from __future__ import annotations
 import argparse
 import copy
 import contextlib
+import gc
 import json
 import os
 import statistics
@@ -232,6 +233,10 @@ def sweep_variants(model_name: str, ctx: int, per_rank_batch: int, dev: torch.de
                          dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         del ddp, opt, model, loss
+        # DDP hooks and the optimizer close reference cycles over the model: without a collection
+        # every variant's 2 B-parameter model stayed allocated (XL world-1 sweep: 138 GiB allocated
+        # after the ZeRO-1 model's init, profiles/r5_ddp_sweep_xl_world1.md)
+        gc.collect()
         if dev.type == "cuda":
             torch.cuda.empty_cache()
         return [float(v) for v in t.tolist()]
@@ -260,10 +265,12 @@ def sweep_variants(model_name: str, ctx: int, per_rank_batch: int, dev: torch.de
             row["skipped"] = "time budget"
         else:
             err = None
+            t_var = time.perf_counter()
             try:
                 st, cw, *_ = run(variant, bucket_mb)
                 row.update(ms_per_step=round(st, 3), comm_wait_ms=round(cw, 3),
-                           comm_fraction=round(cw / st, 4) if st else 0.0)
+                           comm_fraction=round(cw / st, 4) if st else 0.0,
+                           wall_s=round(time.perf_counter() - t_var, 2))
             except Exception as e:  # noqa: BLE001 - reported in the JSON, never loses the headline
                 err = row["error"] = f"{type(e).__name__}: {e}"[:300]
             # every rank exchanges the flag, the failing one included: an error raised at a variant
@@ -282,13 +289,15 @@ def sweep_variants(model_name: str, ctx: int, per_rank_batch: int, dev: torch.de
             mem = {"skipped": "time budget"}
         else:
             try:
+                t_var = time.perf_counter()
                 _, _, m0, mb, ma = run("bucketed", DEFAULT_BUCKET_MB, sharded=True)
                 _, _, r0, rb, ra = run("bucketed", DEFAULT_BUCKET_MB, sharded=False)
+                zero1_wall = round(time.perf_counter() - t_var, 2)
                 mem = {"zero1": {"after_init_mib": round(m0, 1), "peak_before_step_mib": round(mb, 1),
                                  "peak_after_step_mib": round(ma, 1)},
                        "replicated": {"after_init_mib": round(r0, 1), "peak_before_step_mib": round(rb, 1),
                                       "peak_after_step_mib": round(ra, 1)},
-                       "bucket_mb": DEFAULT_BUCKET_MB}
+                       "bucket_mb": DEFAULT_BUCKET_MB, "wall_s": zero1_wall}
             except Exception as e:  # noqa: BLE001
                 mem = {"error": f"{type(e).__name__}: {e}"[:300]}
     return {"model": model_name, "ctx": ctx, "per_rank_batch": per_rank_batch, "steps": steps, "warmup": warmup,

@@ -32,9 +32,12 @@ from .. import ops
 from ..ops import gemm as _gemm
 from ..ops.rope import _normalize_pos
 from ..utils.profiling import annotate
-from . import fused
+from . import compiled, fused
 
 logger = logging.getLogger(__name__)
+
+# tests only: take the torch.compile custom-op path on CPU too (the ops run their reference math)
+_COMPILE_CPU_OPS = False
 
 # "auto": HIP flash attention on GPU, naive on CPU; "naive": always materialize; "flash": always
 # the FA2 path (HIP on GPU, tiled PyTorch on CPU).
@@ -66,6 +69,12 @@ class Linear(nn.Module):
         self.weight = nn.Parameter(_trunc_normal((d_out, d_in), std, device, dtype), requires_grad=True)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if torch.compiler.is_compiling() and (x.is_cuda or _COMPILE_CPU_OPS):
+            # traced by torch.compile: the opaque custom op (models/compiled.py), not the eager
+            # autograd Function (shadow / stream bookkeeping Dynamo cannot trace)
+            cdt = torch.get_autocast_dtype(x.device.type) if torch.is_autocast_enabled(x.device.type) else self.weight.dtype
+            y = compiled.linear(x.reshape(-1, x.shape[-1]), [self.weight], cdt)
+            return y.view(*x.shape[:-1], y.shape[-1])
         if x.is_cuda:
             return fused.fused_linear(x, self.weight)
         return F.linear(x, self.weight)
@@ -102,7 +111,7 @@ class Embedding(nn.Module):
         self.weight = nn.Parameter(_trunc_normal((vocab_size, d_model), 1.0, device, dtype), requires_grad=True)
 
     def forward(self, token_ids: torch.Tensor) -> torch.Tensor:
-        if token_ids.is_cuda and torch.cuda.is_current_stream_capturing():
+        if token_ids.is_cuda and not torch.compiler.is_compiling() and torch.cuda.is_current_stream_capturing():
             return _GraphSafeEmbedding.apply(token_ids, self.weight)
         return F.embedding(token_ids, self.weight)
 
@@ -426,6 +435,8 @@ class BasicsTransformerLM(nn.Module):
     def forward(self, x: torch.Tensor, token_positions: torch.Tensor | None = None) -> torch.Tensor:
         with annotate("embed"):
             h = self.token_embeddings(x)
+        if torch.compiler.is_compiling() and token_positions is None and self._compiled_path_ok(h):
+            return self._forward_compiled(h)
         if self._fused_residual_ok(h):
             return self._forward_fused_residual(h, token_positions)
         for i, layer in enumerate(self.layers):
@@ -457,6 +468,47 @@ class BasicsTransformerLM(nn.Module):
         return all(type(layer).forward is TransformerBlock.forward for layer in self.layers) and all(
             type(n).forward is RMSNorm.forward for n in norms
         )
+
+    def _compiled_path_ok(self, h: torch.Tensor) -> bool:
+        """torch.compile path over the custom ops of models/compiled.py: bf16 autocast (or bf16
+        weights), the stock modules and the grouped QKV / W1|W3 layout (the ops' inputs are the
+        parameters themselves), HIP tensors (or, for the CPU tests, ``_COMPILE_CPU_OPS``)."""
+        if not (len(self.layers) and (h.is_cuda or _COMPILE_CPU_OPS)):
+            return False
+        dev = h.device.type
+        cdt = torch.get_autocast_dtype(dev) if torch.is_autocast_enabled(dev) else self.lm_head.weight.dtype
+        if cdt != torch.bfloat16 or (not self._fused_residual_ok(h) and not _COMPILE_CPU_OPS):
+            return False
+        a0 = self.layers[0].attn
+        return a0.d_k % 8 == 0 and a0.d_k <= 128 and a0.context_parallel is None and all(
+            type(layer.attn).forward is CausalMultiHeadSelfAttention.forward
+            and type(layer.ffn).forward is SwiGLU.forward for layer in self.layers)
+
+    def _forward_compiled(self, h: torch.Tensor) -> torch.Tensor:
+        """The fused-residual block loop of :meth:`_forward_fused_residual` over the custom ops of
+        ``models/compiled.py`` (fused QKV + RoPE GEMM, FA2, output projection, SwiGLU FFN with the
+        gate in the GEMM epilogues), which torch.compile traces with no graph break."""
+        B, N, D = h.shape
+        cos = self.positional_encoder.cos.float().contiguous()
+        sin = self.positional_encoder.sin.float().contiguous()
+        n_layers = len(self.layers)
+        y = self.layers[0].ln1(h)
+        for i, layer in enumerate(self.layers):
+            at = layer.attn
+            qkv = compiled.qkv_rope(y.reshape(B * N, D), [at.q_proj.weight, at.k_proj.weight, at.v_proj.weight],
+                                    cos, sin, N, at.num_heads)
+            o, _ = compiled.attn(qkv.view(B, N, -1), cos, sin, at.num_heads)
+            o = o.transpose(1, 2).reshape(B * N, at.num_heads * at.d_k)
+            a = compiled.linear(o, [at.output_proj.weight], torch.bfloat16).view(B, N, D)
+            self._reading(layer.ln2)
+            h, y = ops.add_rmsnorm(h, a, layer.ln2.weight, layer.ln2.eps)
+            ff = layer.ffn
+            f, _, _ = compiled.swiglu_ffn(y.reshape(B * N, D), ff.w1.weight, ff.w3.weight, ff.w2.weight)
+            nxt = self.layers[i + 1].ln1 if i + 1 < n_layers else self.ln_final
+            self._reading(nxt)
+            h, y = ops.add_rmsnorm(h, f.view(B, N, D), nxt.weight, nxt.eps)
+        logits = compiled.linear(y.reshape(B * N, D), [self.lm_head.weight], torch.bfloat16)
+        return logits.view(B, N, -1)
 
     def _forward_fused_residual(self, h: torch.Tensor, token_positions: torch.Tensor | None) -> torch.Tensor:
         """Same math as the block loop, but each residual add is fused with the norm that reads

@@ -48,6 +48,14 @@ def load_ext() -> bool:
             from . import _fake  # noqa: F401  (registers fake/meta impls for torch.compile)
 
             _loaded = True
+            # explicit Inductor fallbacks for the HIP ops (models/compiled.py explains why); an
+            # optimization of compile time only, so it can never fail the load
+            try:
+                from ..models.compiled import register_inductor_fallbacks
+
+                register_inductor_fallbacks(("cs336",))
+            except Exception:  # noqa: BLE001
+                pass
         except Exception as e:  # pragma: no cover - depends on the box
             _loaded, _load_error = False, f"failed to load {LIB_PATH}: {e!r}"
     return _loaded

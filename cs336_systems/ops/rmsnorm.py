@@ -11,6 +11,8 @@ cast kernel the eager path pays before every projection GEMM. Backward is one fu
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._ext import ops, use_hip
@@ -90,14 +92,15 @@ class AddRMSNormHIP(torch.autograd.Function):
         return dx.view(ctx.shape), dr.view(ctx.shape), dw.to(weight.dtype), None, None
 
 
-def _want_transposed_grad(s: torch.Tensor) -> bool:
-    import os
+# CS336_DYT_FUSED=1: the fused kernel (LDS-staged transposed store) measured 90 us per call vs
+# 60 + 15 us for the row-major kernel plus a separate transpose on XL (-0.5 ms/step), so the
+# two-kernel path is the default. Read once at import (the backward is traced by torch.compile).
+_DYT_FUSED = os.environ.get("CS336_DYT", "1") != "0" and os.environ.get("CS336_DYT_FUSED", "0") != "0"
 
+
+def _want_transposed_grad(s: torch.Tensor) -> bool:
     H, M = s.shape[-1], s.numel() // s.shape[-1]
-    # CS336_DYT_FUSED=1: the fused kernel (LDS-staged transposed store) measured 90 us per call vs
-    # 60 + 15 us for the row-major kernel plus a separate transpose on XL (-0.5 ms/step), so the
-    # two-kernel path is the default
-    if os.environ.get("CS336_DYT", "1") == "0" or os.environ.get("CS336_DYT_FUSED", "0") == "0":
+    if not _DYT_FUSED:
         return False
     rows = 16 if H * 36 <= 65536 else 8
     return s.is_cuda and H % 8 == 0 and H <= 8192 and M % rows == 0
@@ -120,7 +123,7 @@ def add_rmsnorm(x: torch.Tensor, r: torch.Tensor, weight: torch.Tensor, eps: flo
         and x.dtype in (torch.float32, torch.bfloat16)
         and r.dtype in (torch.float32, torch.bfloat16)
         and x.shape == r.shape
-        and torch.result_type(x, r) == x.dtype
+        and (x.dtype == torch.float32 or r.dtype == x.dtype)  # x + r stays in x's dtype (traceable form)
     ):
         if out_dtype is None:
             out_dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
