@@ -232,10 +232,11 @@ def sweep_variants(model_name: str, ctx: int, per_rank_batch: int, dev: torch.de
         t = torch.tensor([statistics.fmean(step_ms), statistics.fmean(comm_ms), mem_init, max(before), max(after)],
                          dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        # the DDP hooks live in the parameters and hold the wrapper and so the model: without
+        # removing them every variant's 2 B-parameter model stayed allocated (XL world-1 sweep: 138
+        # GiB allocated after the ZeRO-1 model's init, profiles/r5_ddp_sweep_xl_world1.md)
+        ddp.remove_hooks()
         del ddp, opt, model, loss
-        # DDP hooks and the optimizer close reference cycles over the model: without a collection
-        # every variant's 2 B-parameter model stayed allocated (XL world-1 sweep: 138 GiB allocated
-        # after the ZeRO-1 model's init, profiles/r5_ddp_sweep_xl_world1.md)
         gc.collect()
         if dev.type == "cuda":
             torch.cuda.empty_cache()

@@ -21,7 +21,8 @@ MI355X/RCCL design notes:
   host never blocks).
 * With the nccl(=RCCL) backend the mean is taken by ``ReduceOp.AVG`` inside the collective; Gloo
   (CPU tests) uses SUM followed by one in-place divide per flat bucket.
-* Bucket cap (``DEFAULT_BUCKET_MB``) — derived, NOT yet measured on a multi-GPU RCCL node. The
+* Bucket cap (``DEFAULT_BUCKET_MB``) — derived, and checked by emulation on one GPU (below); not yet
+  measured on a multi-GPU RCCL node. The
   handout's overhead model prices ``n_b`` buckets of a gradient of ``s`` bytes at
   ``n_b·o + s/(w·n_b)``: a fixed launch/synchronisation cost ``o`` per collective plus the exposed
   all-reduce of the last bucket at algorithm bandwidth ``w``. It is minimal at
@@ -34,7 +35,12 @@ MI355X/RCCL design notes:
   61-127 MB, ``profiles/r3_multirank_rehearsal.jsonl``) and the first all-reduce starts after the
   last layer's backward instead of one and a half layers in; (3) the exposed tail of the last bucket
   stays ≈ 0.75 ms. ``bench.py`` at N > 1 appends an fp32 all-reduce sweep (1/10/100/1024 MB: algbw,
-  busbw) to its JSON, from which ``w`` and ``o`` of the real node refit ``bucket*``.
+  busbw) to its JSON, from which ``w`` and ``o`` of the real node refit ``bucket*``. Measured by
+  emulation on one GPU (``scripts/comm_emulation.py``, ``profiles/r5_ddp_sweep_xl_world1.md``):
+  RCCL-shaped occupants (16 or 32 channel blocks) held for each bucket's W = 8 ring time beside the
+  real XL backward hide all 48 ms/step of communication at 128 MB (598.8 / 599.2 ms/step against
+  599.7 for world-1 DDP), 512 MB exposes the last bucket (+4-8 ms), 32 MB with 32 channels loses
+  52 ms.
 * Unlike the reference, buckets hold only ``requires_grad`` parameters (no empty bucket 0, frozen
   params never block a flush).
 * Collective order is identical on every rank: buckets are issued strictly in index order (a
@@ -132,6 +138,16 @@ class _DDPBase(nn.Module):
 
     def finish_gradient_synchronization(self) -> None:  # pragma: no cover - abstract
         raise NotImplementedError
+
+    def remove_hooks(self) -> None:
+        """Unregister the gradient hooks from the wrapped parameters. The hooks live in the
+        parameters and hold this wrapper (bound methods), which holds the module: a
+        wrapper dropped without this keeps the whole model alive for as long as its parameters are
+        referenced anywhere -- the bench sweep built nine XL models, and seven stayed allocated
+        (``profiles/r5_ddp_sweep_xl_world1.md``)."""
+        for h in self.__dict__.get("_hooks", ()):
+            h.remove()
+        self.__dict__["_hooks"] = []
 
 
 class NaiveDDP(_DDPBase):

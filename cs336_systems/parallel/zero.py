@@ -277,6 +277,12 @@ class ZeroDDP(nn.Module):
         """Bucket indices in the order their reduce-scatters were issued last step (tests)."""
         return list(self._issued)
 
+    def remove_hooks(self) -> None:
+        """Unregister the gradient and forward-pre hooks (see ``DDPBucketed.remove_hooks``)."""
+        for h in list(self.__dict__.get("_hooks", ())) + list(self.__dict__.get("_fwd_hooks", ())):
+            h.remove()
+        self.__dict__["_hooks"], self.__dict__["_fwd_hooks"] = [], []
+
     def finish_gradient_synchronization(self) -> None:
         for b in self.buckets[self._next :]:  # buckets with unused parameters: continue the order
             for p in b.params:

@@ -24,6 +24,7 @@ def main() -> int:
     ap.add_argument("--model", default="xl")
     ap.add_argument("--ctx", type=int, default=512)
     ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--only-bucket", type=float, default=None, help="run only the bucketed variant at this cap (MB)")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29611")
@@ -34,7 +35,10 @@ def main() -> int:
     from cs336_systems.bench.ddp import sweep_variants
 
     t0 = time.perf_counter()
-    out = sweep_variants(a.model, a.ctx, a.batch, dev, budget_s=1e9)
+    kw = {}
+    if a.only_bucket is not None:
+        kw = dict(variants=(("bucketed", a.only_bucket),), zero1=False)
+    out = sweep_variants(a.model, a.ctx, a.batch, dev, budget_s=1e9, **kw)
     out["total_wall_s"] = round(time.perf_counter() - t0, 2)
     print(json.dumps(out), flush=True)
     dist.destroy_process_group()
