@@ -129,6 +129,8 @@ def parse(argv=None):
         help="bucketed DDP / ZeRO-2: dtype of the gradients on the wire (bf16 halves the all-reduce / reduce-scatter bytes)",
     )
     ap.add_argument("--sharded", action="store_true", help="ZeRO-1 sharded optimizer state")
+    ap.add_argument("--ddp-world1", action="store_true",
+                    help="diagnostic: wrap the model in --ddp over a one-rank RCCL group at N = 1 (DDP's own cost)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--clip", type=float, default=0.0, help="global grad-norm clip (0 = off, as the reference bench)")
@@ -322,7 +324,8 @@ def main(argv=None):
 
     ops.set_backend(args.backend)
     zero = args.ddp == "zero"
-    if world > 1 or zero:  # (zero at world 1: a one-rank group, to measure its overhead)
+    dist_on = world > 1 or zero or args.ddp_world1
+    if dist_on:  # (zero / --ddp-world1 at world 1: a one-rank group, to measure the wrapper's overhead)
         # CS336_DIST_BACKEND=gloo: rehearse the multi-rank path with several ranks on one GPU
         rank, world, device = setup_distributed(
             backend=os.environ.get("CS336_DIST_BACKEND") or None, use_gpu=torch.cuda.is_available()
@@ -351,7 +354,7 @@ def main(argv=None):
     if zero:
         zkw = {"comm_dtype": torch.bfloat16} if args.grad_comm_dtype == "bf16" else {}
         ddp_model = ZeroDDP(model, bucket_size_mb=bucket, bf16_shadows=shadows, **zkw, **okw)
-    elif world > 1:
+    elif world > 1 or args.ddp_world1:
         kw = {"comm_dtype": torch.bfloat16} if args.grad_comm_dtype == "bf16" and args.ddp == "bucketed" else {}
         ddp_model = wrap_ddp(model, args.ddp, bucket_size_mb=bucket, **kw)
     else:
@@ -370,7 +373,7 @@ def main(argv=None):
         opt = ops.FusedAdamW(model.parameters(), bf16_shadows=shadows, **okw)
         if overlap:
             # the update of each parameter (DDP: each reduced bucket) runs during backward
-            overlap = opt.enable_backward_overlap(ddp=ddp_model if world > 1 else None)
+            overlap = opt.enable_backward_overlap(ddp=ddp_model if ddp_model is not model else None)
 
     gen = torch.Generator(device=device)
     gen.manual_seed(1000 + rank)
@@ -406,7 +409,7 @@ def main(argv=None):
             logits = ddp_model(x)
             loss = ops.cross_entropy(logits, y)
         loss.backward()
-        if world > 1 or zero:
+        if dist_on:
             if timing["on"] and device.type == "cuda":
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -499,8 +502,8 @@ def main(argv=None):
             "per_gpu_batch": args.batch,
             "seq_len": args.ctx,
             "parallelism": f"dp{world}" + ("+zero2" if zero else "+zero1" if args.sharded and world > 1 else ""),
-            "ddp": args.ddp if world > 1 or zero else "none",
-            "bucket_mb": bucket if world > 1 or zero else None,
+            "ddp": args.ddp if dist_on else "none",
+            "bucket_mb": bucket if dist_on else None,
             "grad_comm_dtype": args.grad_comm_dtype if world > 1 and (args.ddp == "bucketed" or zero) else None,
             "optimizer": "fused HIP AdamW (fp32 master weights)"
             + (", overlapped with backward" if overlap else "")
@@ -521,7 +524,7 @@ def main(argv=None):
     gsel = {"blas": "hipblaslt default", "lt": "autotuned hipblaslt (cs336 lt_gemm)",
             "best": "per-problem fastest of hipblaslt default / autotuned lt_gemm / cs336 MFMA GEMM", "hip": "cs336 MFMA GEMM"}[gemm_mode()]
     out["config"]["gemm_selection"] = f"tunableop:{tmode}" if tmode else gsel if device.type == "cuda" else "torch cpu"
-    if world > 1 or zero:
+    if dist_on:
         out["dist"] = dist_diagnostics(ddp_model, comm_wait_ms, device, world)
         if world > 1 and args.comm_sweep_mb:
             out["dist"]["allreduce_sweep_fp32"] = comm_sweep(args.comm_sweep_mb, device, world)
