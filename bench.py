@@ -103,7 +103,11 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="xl")
     ap.add_argument("--ctx", type=int, default=512)
-    # 96 x 512 = 49152 tokens per GPU (188 GiB of the 288). Per-GPU batch sweep of the XL step on
+    # 102 x 512 = 52224 tokens per GPU (198 GiB of the 288): 204 row tiles of 256, so every d_model-wide
+    # projection output (N 1600 = 5 tiles of 320) fills 1020 of 4 x 256 CU slots instead of 960 at batch
+    # 96 (3.75 rounds, the last a quarter idle). Same box, 2 rounds: 96 -> 87.5-87.6k, 100 -> 88.2k,
+    # 102 -> 88.6k tok/s (profiles/r5_batch102.md; GEMM table and dW plans cover 52224 tokens).
+    # Earlier: 96 x 512 = 49152 tokens per GPU (188 GiB of the 288). Per-GPU batch sweep of the XL step on
     # 1x MI355X with the round-3 kernels (profiles/r3_batch_sweep_s5.md): 48 -> 83.5k, 72 -> 84.3k,
     # 96 -> 85.9-86.1k tok/s -- the per-step fixed costs (fused AdamW over 2.0 B parameters, the
     # vocabulary head, launch tails) amortize over twice the tokens, and under DDP the backward that
@@ -113,7 +117,7 @@ def parse(argv=None):
     # (136 GiB) and 45.6k at 12 x 1024, where every d_model-wide GEMM output has only 384 tiles of
     # 256 x 320 for 256 CUs; profiles/r4_bench_2p7b.md, the committed table covers 12288, 24576 and
     # 32768 tokens)
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: xl 96, 2.7b 32768 tokens / ctx)")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: xl 102, 2.7b 32768 tokens / ctx)")
     ap.add_argument("--vocab", type=int, default=10000)
     ap.add_argument(
         "--ddp",
@@ -187,7 +191,7 @@ def parse(argv=None):
     a = ap.parse_args(argv)
     if a.batch is None:
         env = os.environ.get("CS336_BENCH_BATCH")
-        a.batch = int(env) if env else (max(1, 32768 // a.ctx) if a.model == "2.7b" else 96)
+        a.batch = int(env) if env else (max(1, 32768 // a.ctx) if a.model == "2.7b" else 102)
     return a
 
 

@@ -466,6 +466,12 @@ DW_PLANS: dict = {
     (49152, 4800, 1600): (False, 5),  # QKV: 0.678 (lt 0.950)
     (49152, 1600, 1600): (False, 7),  # O: 0.254 (lt 0.419)
     (49152, 10000, 1600): (False, 5),  # vocabulary head: 1.386 (lt 2.147)
+    # per-GPU batch 102 (52224 tokens, the bench default from round 5): the 49152-token plans
+    (52224, 12800, 1600): (False, 1),
+    (52224, 1600, 6400): (True, 2),
+    (52224, 4800, 1600): (False, 5),
+    (52224, 1600, 1600): (False, 7),
+    (52224, 10000, 1600): (False, 5),
 }
 
 
