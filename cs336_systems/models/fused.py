@@ -586,11 +586,7 @@ class FusedLinearFn(torch.autograd.Function):
                 s.wait_stream(main)
                 with torch.cuda.stream(s):
                     dw = dw_fn(target, True)  # beside the main stream's GEMMs: no stream-K
-                if os.environ.get("CS336_DW_HOLD", "1") == "1":
-                    _hold_for_side(main, s, dy2, x2)
-                else:  # the round-4 form, kept for the A/B (scripts/r4_dws_alloc.sh)
-                    dy2.record_stream(s)
-                    x2.record_stream(s)
+                _hold_for_side(main, s, dy2, x2)
                 if target is None:
                     dw.record_stream(main)
                 _mark_side_work()

@@ -819,46 +819,9 @@ __global__ __launch_bounds__(256) void fa_bwd_delta_kernel(const AttnBwdParams b
   }
 }
 
-// CS336_FA_BWD_CONC=1: delta first, then the dQ kernel on the caller's stream and the dK/dV kernel on a
-// second stream at the same time (each fills the other's causal tail), joined by an event
-inline bool bwd_concurrent() {
-  const char* e = getenv("CS336_FA_BWD_CONC");
-  return e && *e && atoi(e) == 1;
-}
-struct SideStream {
-  hipStream_t st = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-inline SideStream& side_stream() {
-  static SideStream ss[64];
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  SideStream& x = ss[dev & 63];
-  if (x.st == nullptr) {
-    (void)hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking);
-    (void)hipEventCreateWithFlags(&x.fork, hipEventDisableTiming);
-    (void)hipEventCreateWithFlags(&x.join, hipEventDisableTiming);
-  }
-  return x;
-}
-
 template <typename T, int D, bool C, int R, bool DMA>
 void launch_bwd_v(const AttnBwdParams& bp, hipStream_t s, dim3 gq, dim3 gk, dim3 block) {
-  if (bp.ksplit == 1 && bp.qsplit == 1 && bwd_concurrent()) {
-    const AttnParams& p = bp.f;
-    const int64_t rows = (int64_t)p.B * p.H * p.Nq;
-    hipLaunchKernelGGL((fa_bwd_delta_kernel<T, D>), dim3((unsigned)((rows + 127) / 128)), block, 0, s, bp);
-    AttnBwdParams b2 = bp;
-    b2.delta_ready = 1;
-    SideStream& ss = side_stream();
-    (void)hipEventRecord(ss.fork, s);
-    (void)hipStreamWaitEvent(ss.st, ss.fork, 0);
-    hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, C, R, DMA>), gk, block, 0, ss.st, b2);
-    hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, C, R, DMA>), gq, block, 0, s, b2);
-    (void)hipEventRecord(ss.join, ss.st);
-    (void)hipStreamWaitEvent(s, ss.join, 0);
-    return;
-  }
+  // (a two-stream form -- dK/dV beside dQ -- measured slower: profiles/r4_fa_conc.md; retired in round 5)
   hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, C, R, DMA>), gq, block, 0, s, bp);
   hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, C, R, DMA>), gk, block, 0, s, bp);
   const AttnParams& p = bp.f;

@@ -298,11 +298,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
       const bool first = kb == 0, last = kb == kb_last;
       const int qrow = q0 + 32 * qqt + l32;
       float4 pp[4];
-#ifdef CS336_HS_NO_PP  // A/B probe only (wrong dQ): the kernel's time without its dQ partial loads
-      if (false) {
-#else
       if (!first) {
-#endif
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) pp[g4] = *reinterpret_cast<const float4*>(part + qrow * HS_D + 8 * g4);
       }
@@ -395,11 +391,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_hs_kernel(const AttnBwdParams b
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           float v0 = dq[4 * g4], v1 = dq[4 * g4 + 1], v2 = dq[4 * g4 + 2], v3 = dq[4 * g4 + 3];
-#ifdef CS336_HS_NO_PP
-          if (false) {
-#else
           if (!first) {
-#endif
             v0 += pp[g4].x;
             v1 += pp[g4].y;
             v2 += pp[g4].z;

@@ -217,9 +217,6 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
   int dq_row0 = -1;  // first query row of the pending slice (-1: none)
   float* const accb = acc + (int64_t)bh * N * D;
   auto flush_dq = [&]() {
-#ifdef CS336_KP_NO_ATOMICS  // A/B probe only (wrong dQ): the kernel's time without its dQ atomics
-    if (dq_row0 >= -1) return;
-#endif
     if (dq_row0 < 0) return;
 #pragma unroll
     for (int i = 0; i < MT; ++i) {

@@ -437,13 +437,6 @@ bool tile_supported(int bm, int bn) {
 bool gemm_bf16(const GemmArgs& p, int bm, int bn, bool a_kmajor, bool b_kmajor, int out_mode, int splits,
                hipStream_t s) {
   if (!a_kmajor && b_kmajor) return false;  // (MN, K) orientation is not used by the model
-  static const int abl = getenv("CS336_GEMM_ABLATION") ? atoi(getenv("CS336_GEMM_ABLATION")) : 0;
-  if (abl && bm == 256 && bn == 160 && a_kmajor && b_kmajor && out_mode == 0 && splits == 1) {
-    const dim3 grid((unsigned)((p.M / 256) * (p.N / 160))), block(512);
-    if (abl == 1) hipLaunchKernelGGL((gemm_kernel<256, 160, 4, 2, true, true, 0, 1>), grid, block, 0, s, p);
-    else hipLaunchKernelGGL((gemm_kernel<256, 160, 4, 2, true, true, 0, 2>), grid, block, 0, s, p);
-    return true;
-  }
   switch (bm * 1000 + bn) {
     case 256160: return launch_tile<256, 160, 4, 2>(p, a_kmajor, b_kmajor, out_mode, splits, s);
     case 160256: return launch_tile<160, 256, 2, 4>(p, a_kmajor, b_kmajor, out_mode, splits, s);

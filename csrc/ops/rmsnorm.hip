@@ -459,8 +459,6 @@ void rmsnorm_bwd_add(const void* dy, DType dyt, const void* x, DType xt, const f
 namespace cs336 {
 
 int rmsnorm_bwd_add_t_rows(int64_t H) {
-  const char* e = std::getenv("CS336_DYT_ROWS");  // A/B: 8 or 16 rows per workgroup
-  if (e && std::atoi(e) == 8) return 8;
   return H * 18 * 2 <= 65536 ? 16 : 8;
 }
 

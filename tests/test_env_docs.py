@@ -1,0 +1,51 @@
+"""Configuration hygiene: every ``CS336_*`` environment variable the library, the
+native code and ``bench.py`` read is documented in README's environment table; every ``CS336_*``
+build define the kernels test is in README's build-switch table; and no kernel source carries a
+probe switch that produces wrong results (those live as patches in ``scripts/variants/``)."""
+
+import pathlib
+import re
+
+REPO = pathlib.Path(__file__).resolve().parents[1]
+CODE = [REPO / "cs336_systems", REPO / "csrc", REPO / "bench.py", REPO / "__graft_entry__.py"]
+
+
+def _files():
+    for root in CODE:
+        if root.is_file():
+            yield root
+        else:
+            yield from (f for f in root.rglob("*") if f.suffix in (".py", ".cpp", ".hip", ".h"))
+
+
+def _readme():
+    return (REPO / "README.md").read_text()
+
+
+def test_every_env_switch_is_documented():
+    names = set()
+    for f in _files():
+        names |= set(re.findall(r"[\"'](CS336_[A-Z0-9_]+)[\"']", f.read_text(errors="ignore")))
+    table = "\n".join(line for line in _readme().splitlines() if line.startswith("| `CS336_"))
+    missing = sorted(n for n in names if f"`{n}" not in table and f", `{n}" not in table and f"{n}=" not in table)
+    assert not missing, f"undocumented CS336_* environment switches: {missing}"
+
+
+def test_every_build_define_is_documented():
+    defines = set()
+    for f in _files():
+        defines |= set(re.findall(r"#\s*if(?:n?def)?\s+(?:defined\()?\s*(CS336_[A-Z0-9_]+)", f.read_text(errors="ignore")))
+    readme = _readme()
+    missing = sorted(d for d in defines if f"`{d}" not in readme)
+    assert not missing, f"undocumented CS336_* build defines: {missing}"
+
+
+def test_no_wrong_result_probe_in_kernels():
+    bad = []
+    for f in (REPO / "csrc").rglob("*"):
+        if f.suffix not in (".hip", ".h", ".cpp"):
+            continue
+        for i, line in enumerate(f.read_text(errors="ignore").splitlines(), 1):
+            if re.match(r"\s*#\s*if", line) and "wrong" in line.lower():
+                bad.append(f"{f.relative_to(REPO)}:{i}")
+    assert not bad, bad

@@ -193,26 +193,3 @@ def test_split_backward_matches(dt, causal, N, D, monkeypatch):
         err = (a.double() - r).abs().max().item()
         assert err <= tol * max(1.0, r.abs().max().item()), (name, err)
         torch.testing.assert_close(a.float(), b.float(), rtol=tol, atol=tol)
-
-
-@pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("D", [64, 128])
-def test_two_kernel_concurrent_matches(causal, D, monkeypatch):
-    """CS336_FA_BWD_CONC=1: delta by its own kernel, then the dQ and dK/dV kernels on two streams at
-    once -- bitwise the serial two-kernel result (same delta summation order)."""
-    from cs336_systems.ops._ext import ops as _hip
-
-    torch.manual_seed(7)
-    B, H, N = 2, 4, 1024
-    mk = lambda: torch.randn(B, N, H, D, device="cuda", dtype=torch.bfloat16).transpose(1, 2)  # noqa: E731
-    q, k, v, do = mk(), mk(), mk(), mk()
-    hip = _hip()
-    o, lse = hip.fa_fwd(q, k, v, causal, D**-0.5)
-    monkeypatch.setenv("CS336_FA_BWD", "0")
-    monkeypatch.setenv("CS336_FA_BWD_SPLITS", "1")
-    ref = hip.fa_bwd(do, q, k, v, o, lse, causal, D**-0.5)
-    monkeypatch.setenv("CS336_FA_BWD_CONC", "1")
-    got = hip.fa_bwd(do, q, k, v, o, lse, causal, D**-0.5)
-    torch.cuda.synchronize()
-    for a, b in zip(got, ref):
-        assert torch.equal(a, b)
