@@ -125,15 +125,17 @@ def _pick(kind: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None,
             # wider run: (2560, 20480) with ld 665360 on the 2.7b): the table's dense-layout pick
             t = selection_table().get(str(_dense_key(key)))
         if t is not None and t in cands:
+            t = _multi_rank_safe(t, cands)
             _BEST[key] = t
             _BEST_TIMES[key] = {"table": t}
             return t
         if torch.cuda.is_current_stream_capturing():
             return "blas"
         if _multi_rank():
-            _BEST[key] = "blas"
-            _BEST_TIMES[key] = {"untimed_multi_rank": "blas"}
-            return "blas"
+            t = _multi_rank_safe("blas", cands)
+            _BEST[key] = t
+            _BEST_TIMES[key] = {"untimed_multi_rank": t}
+            return t
         # the partials of a split-K candidate are extra memory at the selection step (first step,
         # inside backward): time one only with room to spare; free memory is queried
         # here, on a cache miss, not on every call
@@ -151,6 +153,20 @@ def _pick(kind: str, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None,
 
 
 _BEST_TIMES: dict = {}
+
+
+def _multi_rank_safe(pick: str, cands: dict) -> str:
+    """In a multi-rank job a hipBLASLt pick ("lt" / "blas") is replaced by a cs336 kernel where one
+    applies (gemm8, else the older cs336 GEMM): hipBLASLt's picks for these shapes are stream-K
+    kernels whose workgroups wait on later workgroups of their grid, the hazard beside RCCL
+    collectives that ``cs336_systems/rccl_env.py`` describes, while every cs336 workgroup owns whole
+    tiles and never waits for another. It costs the 2.7b table's four hipBLASLt picks 1-10 % each
+    (``profiles/r5_gemm_2p7b.md``) and only in multi-rank runs; single-GPU runs keep the fastest."""
+    if pick in ("lt", "blas") and _multi_rank():
+        for alt in ("g8", "cs336"):
+            if alt in cands:
+                return alt
+    return pick
 
 
 def _dense_key(key: tuple) -> tuple:

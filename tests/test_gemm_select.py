@@ -57,3 +57,24 @@ def test_ample_free_memory_times_split_k(monkeypatch):
 def test_near_tie_prefers_blas(monkeypatch):
     pick, _ = _run(monkeypatch, 1 << 30, {"blas": 1.0, "lt": 0.99, "cs336_sk": 0.1})
     assert pick == "blas"
+
+
+def test_multi_rank_replaces_hipblaslt_table_pick(monkeypatch):
+    """A committed "lt" / "blas" pick becomes the cs336 kernel in a multi-rank job (stream-K beside RCCL)."""
+    monkeypatch.setattr(gemm, "_BEST", {})
+    monkeypatch.setattr(gemm, "_BEST_TIMES", {})
+    a, b = torch.empty(256, 64), torch.empty(64, 64)
+    key = ("nt", tuple(a.shape), a.stride(), tuple(b.shape), b.stride(), None)
+    monkeypatch.setattr(gemm, "selection_table", lambda: {str(key): "lt"})
+    cands = {"blas": lambda: None, "lt": lambda: None, "g8": lambda: None}
+    monkeypatch.setattr(gemm, "_multi_rank", lambda: True)
+    assert gemm._pick("nt", a, b, None, cands) == "g8"
+    monkeypatch.setattr(gemm, "_BEST", {})
+    monkeypatch.setattr(gemm, "_multi_rank", lambda: False)
+    assert gemm._pick("nt", a, b, None, cands) == "lt"
+    # an untimed multi-rank miss: the cs336 kernel too
+    monkeypatch.setattr(gemm, "_BEST", {})
+    monkeypatch.setattr(gemm, "selection_table", lambda: {})
+    monkeypatch.setattr(gemm, "_multi_rank", lambda: True)
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
+    assert gemm._pick("nt", a, b, None, {"blas": lambda: None, "cs336": lambda: None}) == "cs336"
