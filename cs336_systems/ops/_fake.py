@@ -111,6 +111,13 @@ def _rope_into(x, cos, sin, pos, inverse, out):
     return None
 
 
+if hasattr(torch.ops.cs336, "splitk_sum"):  # (absent from libraries built before round 5: A/B baselines)
+
+    @register_fake("cs336::splitk_sum")
+    def _splitk_sum(slabs, out, accumulate):
+        return None
+
+
 @register_fake("cs336::swiglu_fused_fwd")
 def _swiglu_fused_fwd(y):
     return y.new_empty((*y.shape[:-1], y.shape[-1] // 2))

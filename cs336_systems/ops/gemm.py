@@ -561,7 +561,9 @@ def mm_dw(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None, ac
         return out.add_(tmp) if accumulate else out.copy_(tmp)
     slabs = torch.empty(sk, n_out, k_in, device=dy.device, dtype=torch.float32)
     ops().gemm8w(a, b, slabs, sk, trans, False, 0)
-    if accumulate:
+    if direct and k_in % 4 == 0:
+        ops().splitk_sum(slabs, out, accumulate)  # one pass over the slabs (torch.sum's dim-0 reduce: ~2.5x slower)
+    elif accumulate:
         out.add_(slabs.sum(0))
     else:
         torch.sum(slabs, dim=0, out=out)

@@ -1096,6 +1096,24 @@ void gemm8w(const at::Tensor& a, const at::Tensor& b, at::Tensor& out, int64_t s
   }
 }
 
+// Sum of split-K fp32 slabs (splits, M, N) into out (M, N; unit column stride, 16-B aligned rows),
+// optionally added to it: one float4 per thread walking the splits (csrc/gemm/gemm.hip). Replaces
+// torch.sum(slabs, 0), whose generic dim-0 reduction ran at ~40 % of HBM for the weight gradients'
+// slabs (profiles/r5_2p7b_roofline_b32.md: 75.6 us per 2560 x 2560 call).
+void splitk_sum(const at::Tensor& slabs, at::Tensor& out, bool accumulate) {
+  TORCH_CHECK(slabs.is_cuda() && slabs.scalar_type() == at::kFloat && slabs.dim() == 3 && slabs.is_contiguous(),
+              "cs336: splitk_sum slabs must be contiguous fp32 (splits, M, N)");
+  const int64_t M = slabs.size(1), N = slabs.size(2);
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.dim() == 2 && out.size(0) == M &&
+                  out.size(1) == N && out.stride(1) == 1 && out.stride(0) % 4 == 0 && N % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "cs336: splitk_sum out must be fp32 (M, N) with 16-B aligned rows");
+  if (M * N == 0 || slabs.size(0) == 0) return;
+  c10::DeviceGuard g(slabs.device());
+  cs336::gemm::splitk_reduce(slabs.data_ptr<float>(), out.data_ptr<float>(), M, N, (int)slabs.size(0), out.stride(0),
+                             accumulate, stream());
+}
+
 TORCH_LIBRARY(cs336, m) {
   m.def(
       "fa_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None, "
@@ -1144,6 +1162,7 @@ TORCH_LIBRARY(cs336, m) {
   m.def("gemm8_stagger(int epi, int ticks, int groups) -> bool", &gemm8_stagger);
   m.def("gemm8_rope(Tensor a, Tensor b, Tensor(a!) c, Tensor cos, Tensor sin, Tensor? pos, int seq, int rope_cols, int dhead) -> ()");
   m.def("gemm8w(Tensor a, Tensor b, Tensor(a!) out, int splits, bool trans_out, bool accumulate, int fn) -> ()");
+  m.def("splitk_sum(Tensor slabs, Tensor(a!) out, bool accumulate) -> ()");
   m.def("multi_tensor_scale_(Tensor(a!)[] tensors, Tensor scale) -> ()");
 }
 
@@ -1178,5 +1197,6 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("gemm8", &gemm8);
   m.impl("gemm8_rope", &gemm8_rope);
   m.impl("gemm8w", &gemm8w);
+  m.impl("splitk_sum", &splitk_sum);
   m.impl("multi_tensor_scale_", &multi_tensor_scale_);
 }

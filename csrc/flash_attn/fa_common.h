@@ -40,6 +40,18 @@ constexpr float kRescaleThr = 8.f;
 // raw v_exp_f32 (2^x); exp2f() adds a denormal-range fixup sequence we do not need here
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// ---- lane halves: v_permlane32_swap (guide T12 / T21) ------------------------------------------
+// lane i's value combined with lane i ^ 32's by one half swap, instead of a ds_bpermute round trip
+// (__shfl_xor(x, 32)); both operations are commutative, so every lane gets the same bits as before
+__device__ __forceinline__ float xhalf_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // wave index as a provably wave-uniform (SGPR) value, so per-wave tile skips / mask decisions
 // compile to scalar branches instead of predicated vector code
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }

@@ -37,6 +37,16 @@ constexpr int fwd_min_waves() {
   return std::is_same<T, float>::value ? 1 : 2;
 }
 
+// the PV loop's prefetched V^T fragment type (16-bit only; a placeholder for fp32)
+template <typename T, bool ON>
+struct VFrag {
+  typedef int type;
+};
+template <typename T>
+struct VFrag<T, true> {
+  typedef typename Mma16<T>::frag type;
+};
+
 // DMA: 0 = VGPR staging, 1 = LDS-DMA ring of K|V tiles, 2 = LDS-DMA into separate K and V rings
 // with the next tile's S^T MFMAs issued inside the current tile's softmax (software pipeline)
 template <typename T, int D, bool CAUSAL, bool ROPE, int DMA>
@@ -147,6 +157,22 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
   auto active = [&](int j) { return !CAUSAL || (jt0 + j) * BN <= qw0 + 31; };
   auto s_tile = [&](const char* Ks, f32x16 (&s)[2]) {
     // ---- S^T = K Q^T ----
+    if constexpr (!F32 && DP <= 64) {
+      // every K fragment of the tile read before the first MFMA (<= 32 VGPRs): the MFMA chain then
+      // waits on one LDS round trip instead of one per fragment
+      typename Mma16<T>::frag kf[2][DP / 16];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ks = 0; ks < DP / 16; ++ks) kf[t][ks] = lds_row_frag<T, RB>(Ks, 32 * t, ks, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        s[t] = zero16();
+#pragma unroll
+        for (int ks = 0; ks < DP / 16; ++ks) s[t] = Mma16<T>::mma(kf[t][ks], as_frag<T>(qf[ks]), s[t]);
+      }
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       s[t] = zero16();
@@ -172,13 +198,14 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
     // ---- mask (bounds / causal diagonal) ----
     const bool need_mask = (kt0 + BN > p.Nk) || (CAUSAL && kt0 + BN - 1 > qw0);
     if (need_mask) {
+      // key = kt0 + 32t + acc_row(r, hh) is masked iff it exceeds min(Nk - 1, qrow): one compare of
+      // a constant against a per-lane limit per element
+      const int lim = (CAUSAL ? min(p.Nk - 1, qrow) : p.Nk - 1) - kt0 - 4 * hh;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kt0 + 32 * t + acc_row(r, hh);
-          if (key >= p.Nk || (CAUSAL && key > qrow)) s[t][r] = -INFINITY;
-        }
+        for (int r = 0; r < 16; ++r)
+          if (32 * t + acc_row(r, 0) > lim) s[t][r] = -INFINITY;
     }
     // ---- online softmax (query on the lane), deferred rescale (T13) ----
     float mx = s[0][0];
@@ -186,7 +213,7 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[t][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = xhalf_max(mx);
     const float mt = mx * c2;
     if (__ballot(mt > m + kRescaleThr) != 0) {  // wave-uniform
       const float m_new = fmaxf(m, mt);
@@ -199,6 +226,21 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
         for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
     }
     mid();
+    // 16-bit causal LDS-DMA kernel, d <= 64: the tile's V^T fragments (<= 32 VGPRs) are requested
+    // before the exp2 loop, so their LDS round trip runs under it instead of in front of every PV
+    // MFMA: +9 % at N 4096 d 64 (707 -> 771 TF), +1.5 % at the XL step's N 512 (profiles/r5_fa_fwd.md).
+    // Not without the mask: there the extra registers (163 -> 187) cost a wave per SIMD (-4 %)
+    constexpr bool VPRE = !F32 && DP <= 64 && DMA == 1 && CAUSAL;
+    typename VFrag<T, VPRE>::type vf[VPRE ? NDT : 1][2][2];
+    if constexpr (VPRE) {
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) vf[dt][t][s2] = lds_tr_frag<T, RB>(Vs, 32 * t, s2, dt, lane);
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads here (the scheduler sinks them to their MFMAs)
+    }
     float rs = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -231,7 +273,8 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2)
-            o[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Vs, 32 * t, s2, dt, lane), pf[t][s2], o[dt]);
+            if constexpr (VPRE) o[dt] = Mma16<T>::mma(vf[dt][t][s2], pf[t][s2], o[dt]);
+            else o[dt] = Mma16<T>::mma(lds_tr_frag<T, RB>(Vs, 32 * t, s2, dt, lane), pf[t][s2], o[dt]);
     }
   };
   auto tile = [&](int j, const char* Ks) __attribute__((always_inline)) {
@@ -377,7 +420,7 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
   // ---- epilogue ----
   // (an empty key split of the DMA-2 ring issued its prologue and never reached the draining `last`)
   if constexpr (DMA == 2) wait_vmcnt<0>();
-  l += __shfl_xor(l, 32, 64);
+  l = xhalf_sum(l);
   const float inv = l > 0.f ? 1.f / l : 0.f;
   if (nsplit > 1) {
     // split-KV partial: normalized fp32 O of this key range and its natural-log LSE (merge kernel)
@@ -399,15 +442,42 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
   }
   if (valid_q) {
     S* orow = Op + (int64_t)qrow * p.o_sn;
+    // 16-bit O with 16-B aligned rows (T21): lane half hh holds d 8g+4hh .. +3 of its row per register
+    // group g; one v_permlane32_swap per dword pairs groups (g, g+1), after which lanes 0-31 hold d
+    // 8g .. 8g+7 and lanes 32-63 d 8g+8 .. 8g+15 of the same row: one 16-B store where there were two
+    // 8-B stores (the per-block store tail is issue-bound)
+    bool wide = false;
+    if constexpr (!F32) wide = ((p.o_sn | p.o_sb | p.o_sh) & 7) == 0 && ((uintptr_t)p.o & 15) == 0;
+    if constexpr (!F32) if (wide) {
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
+      for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * hh;
-        if (DP == D || d < D)
-          store4<T>(orow + d, make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
-                                          o[dt][4 * g + 3] * inv));
-      }
+        for (int g = 0; g < 4; g += 2) {
+          uint32_t c[4];
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int r0 = 4 * g + 2 * k;
+            const uint32_t lo = (uint32_t)Elem<T>::from_f(o[dt][r0] * inv) | ((uint32_t)Elem<T>::from_f(o[dt][r0 + 1] * inv) << 16);
+            const uint32_t hi = (uint32_t)Elem<T>::from_f(o[dt][r0 + 4] * inv) | ((uint32_t)Elem<T>::from_f(o[dt][r0 + 5] * inv) << 16);
+            const auto sw = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+            c[k] = sw[0];
+            c[2 + k] = sw[1];
+          }
+          const int d = dt * 32 + 8 * g + 8 * hh;
+          if (DP == D || d < D) *reinterpret_cast<uint4*>(orow + d) = make_uint4(c[0], c[1], c[2], c[3]);
+        }
+    }
+    if (!wide) {
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = dt * 32 + 8 * g + 4 * hh;
+          if (DP == D || d < D)
+            store4<T>(orow + d, make_float4(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv,
+                                            o[dt][4 * g + 3] * inv));
+        }
+    }
 
     if (hh == 0) p.lse[((int64_t)b * p.H + h) * p.Nq + qrow] = l > 0.f ? (m + __log2f(l)) * kLn2 : -INFINITY;
   }
@@ -567,6 +637,7 @@ size_t flash_attn_fwd_split_workspace(const AttnParams& p, int splits) {
 
 void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s) {
   if (p.B * p.H == 0 || p.Nq == 0) return;
+  if (flash_attn_fwd_multi(p, t, s)) return;  // many short heads: the persistent multi-item kernel
   switch (t) {
     case DType::BF16: fa::launch_fwd_d<BF16>(p, s); break;
     case DType::F16: fa::launch_fwd_d<F16>(p, s); break;

@@ -58,14 +58,18 @@ def main():
     work = {  # kernel -> (kind, amount): FLOPs or bytes for the whole step
         "GEMM fwd": ("F", gemm_fwd),
         "GEMM bwd (dX + dW)": ("F", 2 * gemm_fwd),
-        "FA fwd": ("F", L * attn_fwd),
-        "FA bwd (dq + dkdv)": ("F", L * 2.5 * attn_fwd),
+        # attention: FLOPs AND bytes (q, k, v read + o written; the backward reads q, k, v, o, dO and
+        # writes dq, dk, dv, all bf16, + fp32 row constants): at N 512-1024 the byte time is the larger
+        "FA fwd": ("FB", (L * attn_fwd, L * (4 * M * d * 2 + M * H * 4))),
+        "FA bwd (dq + dkdv)": ("FB", (L * 2.5 * attn_fwd, L * (8 * M * d * 2 + 2 * M * H * 4))),
         "rmsnorm_fwd_kernel": ("B", 2 * L * M * d * 12),  # x f32 + r bf16 in, s f32 + y bf16 out
         "rmsnorm_bwd_kernel": ("B", 2 * L * M * d * 16),  # dy bf16, x f32, dres f32 in; dx f32 + bf16 out
         "silu_mul_fwd_kernel": ("B", L * M * f * 6),
         "silu_mul_bwd_kernel": ("B", L * M * f * 10),
         "rope_kernel": ("B", L * M * 2 * d * 2 * 2),  # q|k bf16 read + write (d each)
         "adamw_kernel": ("B", P * 30),  # p,g,m,v in; p,m,v + bf16 shadow out
+        # the 2-D weights' update (all but the 2L + 1 norm vectors): + the bf16 Wᵀ shadow
+        "adamw_t_kernel": ("B", (P - (2 * L + 1) * d) * 32),
         "transpose16_kernel": ("B", None),
     }
     total = sum(t.values())
@@ -76,7 +80,14 @@ def main():
         if ms < 0.3:
             continue
         kind, amt = work.get(k, (None, None))
-        if kind == "F":
+        if kind == "FB":
+            fl, by = amt
+            tf, tb = fl / (ms * 1e-3) / 1e12, by / (ms * 1e-3) / 1e12
+            bound = max(fl / PEAK_TF, by / PEAK_TBS) / 1e12 * 1e3  # ms at the binding roof
+            which = "HBM" if by / PEAK_TBS > fl / PEAK_TF else "MFMA"
+            print(f"| {k} | {n[k]} | {ms:.1f} | {tf:.0f} TFLOP/s, {tb:.2f} TB/s | {bound:.1f} ms ({which}-bound) | "
+                  f"{100 * bound / ms:.0f} % |")
+        elif kind == "F":
             ach = amt / (ms * 1e-3) / 1e12
             print(f"| {k} | {n[k]} | {ms:.1f} | {ach:.0f} TFLOP/s | {PEAK_TF:.0f} TFLOP/s dense bf16 | {100 * ach / PEAK_TF:.0f} % |")
         elif kind == "B" and amt:

@@ -128,3 +128,19 @@ def test_gemm8_tail_strided():
     c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     cs.gemm8(a, b, c, 0, 0, None, None, 0)
     assert _rel(c, a.float() @ b.float().t()) < 5e-3
+
+
+@pytest.mark.parametrize("S,M,N,acc", [(4, 256, 320, False), (2, 1600, 1600, True), (8, 64, 2560, False)])
+def test_splitk_sum(S, M, N, acc):
+    """splitk_sum (the weight gradients' split-K slab reduction) against torch.sum in fp32, into a
+    strided row-padded output, plain and accumulating."""
+    cs = _cs()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    slabs = torch.randn(S, M, N, device="cuda", generator=g)
+    base = torch.randn(M, N + 4, device="cuda", generator=g)
+    out = base.clone()
+    view = out[:, :N]
+    cs.splitk_sum(slabs, view, acc)
+    ref = slabs.sum(0) + (base[:, :N] if acc else 0)
+    torch.testing.assert_close(view, ref, rtol=1e-6, atol=1e-5)
+    assert torch.equal(out[:, N:], base[:, N:])  # the row padding is untouched
