@@ -36,7 +36,7 @@ MI355X/RCCL design notes:
   last layer's backward instead of one and a half layers in; (3) the exposed tail of the last bucket
   stays ≈ 0.75 ms. ``bench.py`` at N > 1 appends an fp32 all-reduce sweep (1/10/100/1024 MB: algbw,
   busbw) to its JSON, from which ``w`` and ``o`` of the real node refit ``bucket*``. Measured by
-  emulation on one GPU (``scripts/comm_emulation.py``, ``profiles/r5_ddp_sweep_xl_world1.md``):
+  emulation on one GPU (``scripts/comm_emulation.py``, ``profiles/r5_comm_emulation.md``):
   RCCL-shaped occupants (16 or 32 channel blocks) held for each bucket's W = 8 ring time beside the
   real XL backward hide all 48 ms/step of communication at 128 MB (598.8 / 599.2 ms/step against
   599.7 for world-1 DDP), 512 MB exposes the last bucket (+4-8 ms), 32 MB with 32 channels loses
