@@ -637,7 +637,6 @@ size_t flash_attn_fwd_split_workspace(const AttnParams& p, int splits) {
 
 void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s) {
   if (p.B * p.H == 0 || p.Nq == 0) return;
-  if (flash_attn_fwd_multi(p, t, s)) return;  // many short heads: the persistent multi-item kernel
   switch (t) {
     case DType::BF16: fa::launch_fwd_d<BF16>(p, s); break;
     case DType::F16: fa::launch_fwd_d<F16>(p, s); break;

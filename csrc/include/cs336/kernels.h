@@ -186,8 +186,6 @@ struct AttnBwdParams {
 void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s);
 // key splits the forward uses for p (1 = none) and the fp32 workspace they need (floats)
 int flash_attn_fwd_splits(const AttnParams& p);
-// persistent multi-item forward (fa_fwd_multi.hip): launches and returns true where it applies
-bool flash_attn_fwd_multi(const AttnParams& p, DType t, hipStream_t s);
 size_t flash_attn_fwd_split_workspace(const AttnParams& p, int splits);
 void flash_attn_bwd(const AttnBwdParams& p, DType t, hipStream_t s);
 // (ksplit, qsplit) the two-kernel backward uses for p at low parallelism, and their fp32 workspace
