@@ -249,7 +249,8 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
   // CS336_FA_BWD selects the backward:
   //   unset: a head-sequential kernel where it applies and the (batch, head) workgroups fill the chip
   //          (B·H >= 512): fa_bwd_hs.hip (d 64, N <= 1024, N % 128 == 0), else fa_bwd_fused.hip
-  //          (d 64, N <= 1024); else at d 80 the key-block-parallel fused
+  //          (d 64, N <= 1024: the N % 128 == 64 shapes, 1.37x the two-kernel form,
+  //          profiles/r5_fa_bwd_forms.md); else at d 80 the key-block-parallel fused
   //          kernel (fa_bwd_kp.hip, dQ by fp32 atomics), else the two-kernel form (split over keys /
   //          queries at low parallelism);
   //   1: head-sequential wherever it applies (then as unset); 2: key-block parallel wherever it
