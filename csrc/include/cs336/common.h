@@ -79,6 +79,37 @@ __device__ __forceinline__ void store4(typename Elem<T>::storage* p, float4 v) {
   }
 }
 
+// Non-temporal forms (the `nt` cache-policy bit: the line is streamed, not kept for reuse) for tensors
+// touched once now and next only after other work has cycled the caches -- the fp32 residual stream
+// and its gradient (csrc/ops/rmsnorm.hip), so that the bf16 operands the next GEMM reads stay cached.
+typedef __attribute__((ext_vector_type(4))) float cs336_f32x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned int cs336_u32x2_t;
+template <typename T>
+__device__ __forceinline__ float4 load4_nt(const typename Elem<T>::storage* p) {
+  if constexpr (sizeof(typename Elem<T>::storage) == 4) {
+    const cs336_f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const cs336_f32x4_t*>(p));
+    return make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    const cs336_u32x2_t u = __builtin_nontemporal_load(reinterpret_cast<const cs336_u32x2_t*>(p));
+    typedef typename Elem<T>::storage S;
+    S s0 = (S)(u[0] & 0xffff), s1 = (S)(u[0] >> 16), s2 = (S)(u[1] & 0xffff), s3 = (S)(u[1] >> 16);
+    return make_float4(Elem<T>::to_f(s0), Elem<T>::to_f(s1), Elem<T>::to_f(s2), Elem<T>::to_f(s3));
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store4_nt(typename Elem<T>::storage* p, float4 v) {
+  if constexpr (sizeof(typename Elem<T>::storage) == 4) {
+    cs336_f32x4_t w;
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    __builtin_nontemporal_store(w, reinterpret_cast<cs336_f32x4_t*>(p));
+  } else {
+    cs336_u32x2_t w;
+    w[0] = (uint32_t)Elem<T>::from_f(v.x) | ((uint32_t)Elem<T>::from_f(v.y) << 16);
+    w[1] = (uint32_t)Elem<T>::from_f(v.z) | ((uint32_t)Elem<T>::from_f(v.w) << 16);
+    __builtin_nontemporal_store(w, reinterpret_cast<cs336_u32x2_t*>(p));
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // wave64 / block reductions
 // ------------------------------------------------------------------------------------------

@@ -37,11 +37,14 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const typename Elem<TX
   for (int k = 0; k < NV; ++k) {
     const int i = lane + kWave * k;
     if (i < H4) {
-      v[k] = load4<TX>(xr + 4 * i);
+      // ADD (pre-norm residual): the stream x comes from a sublayer ago and s is read next a sublayer
+      // from now (and in the backward): both stream past the caches (nt), which keeps the bf16 branch
+      // output r (just written by a GEMM) and y (read next by a GEMM) cached
+      v[k] = ADD ? load4_nt<TX>(xr + 4 * i) : load4<TX>(xr + 4 * i);
       if constexpr (ADD) {
         const float4 rv = load4<TR>(res + row * H + 4 * i);
         v[k].x += rv.x; v[k].y += rv.y; v[k].z += rv.z; v[k].w += rv.w;
-        store4<TX>(s + row * H + 4 * i, v[k]);
+        store4_nt<TX>(s + row * H + 4 * i, v[k]);
         // normalize what was stored (rounded to TX), like the unfused add -> rmsnorm
         if constexpr (!std::is_same<TX, float>::value) {
           v[k].x = Elem<TX>::to_f(Elem<TX>::from_f(v[k].x));
@@ -110,9 +113,11 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const typename Elem<TD
     for (int k = 0; k < NV; ++k) {
       const int i = lane + kWave * k;
       if (i < H4) {
-        xv[k] = load4<TX>(xr + 4 * i);
+        // ADD: the saved stream x and the residual gradient dres (a sublayer old) stream past the
+        // caches; dy (just written by a GEMM) is read normally
+        xv[k] = ADD ? load4_nt<TX>(xr + 4 * i) : load4<TX>(xr + 4 * i);
         gv[k] = load4<TDY>(dyr + 4 * i);
-        if constexpr (ADD) dv[k] = load4<TX>(dres + row * H + 4 * i);
+        if constexpr (ADD) dv[k] = load4_nt<TX>(dres + row * H + 4 * i);
       } else {
         xv[k] = gv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (ADD) dv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -138,7 +143,8 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const typename Elem<TD
           o.x += dv[k].x; o.y += dv[k].y; o.z += dv[k].z; o.w += dv[k].w;
           if (dx2) store4<BF16>(dx2 + row * H + 4 * i, o);
         }
-        store4<TX>(dxr + 4 * i, o);
+        if constexpr (ADD) store4_nt<TX>(dxr + 4 * i, o);  // (read next a sublayer from now)
+        else store4<TX>(dxr + 4 * i, o);
         dwp[k].x += gv[k].x * xv[k].x * r;
         dwp[k].y += gv[k].y * xv[k].y * r;
         dwp[k].z += gv[k].z * xv[k].z * r;
