@@ -144,10 +144,12 @@ def parse(argv=None):
     ap.add_argument("--no-fused-layout", action="store_true", help="separate q/k/v and w1/w3 GEMMs (A/B)")
     ap.add_argument(
         "--overlap-opt",
-        default="off",
+        default="auto",
         choices=["auto", "on", "off"],
-        # measured on 1x MI355X (XL, batch 24): 189.2 ms/step off vs 193.0 on: backward already keeps
-        # the GPU 97 % busy, so the HBM-bound update only competes with the GEMMs (profiles/README.md)
+        # XL at batch 102 (round 5, same box, 3 rounds): 576.7 / 577.1 / 577.3 ms/step overlapped vs
+        # 580.8 / 580.9 / 582.6 off (profiles/r5_opt_overlap_ab.md): the HBM-bound update of each
+        # layer's weights runs beside the next layers' backward. (Round 1, batch 24 and the older
+        # kernels: 193.0 on vs 189.2 off.) Bitwise the same update (tests/test_opt_overlap_gpu.py)
         help="run the AdamW update during backward on a side stream (auto: on GPU when clip == 0 and not sharded)",
     )
     ap.add_argument(
