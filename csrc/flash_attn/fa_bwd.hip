@@ -757,31 +757,54 @@ CS336_FA_BWD_DMA(F16, 80)
 CS336_FA_BWD_DMA(F16, 128)
 #undef CS336_FA_BWD_DMA
 
-// sum of `ns` unscaled fp32 split partials ([split][B·H][N][D]) -> out (B, H, N, D strided) = scale ·
-// sum, rotated back by RoPE when `rope` (dQ/dK w.r.t. the un-rotated q/k); one thread per 4 d
+// One split-partial reduction: `ns` unscaled fp32 partials ([split][B·H][N][D]) -> out (B, H, N, D
+// strided) = scale · sum, rotated back by RoPE when rcos (dQ/dK w.r.t. the un-rotated q/k)
+struct SplitSum {
+  const float* part;
+  int ns, N;
+  void* out;
+  int64_t sb, sh, sn;
+  float scale;
+  const float* rcos;
+  const float* rsin;
+  const int64_t* rpos;
+  int64_t units;  // B·H·N·D/4 (0: nothing to reduce)
+};
+
+// dQ, dK and dV split sums in ONE launch (three launches cost ~4 us each at the B 1 H 1 sizes the
+// split serves); one thread per 4 d, partials summed in split order. An in-launch form (the dK/dV
+// kernel summing dQ, its last-arriving split summing dK/dV) measured 1.3-2.7x slower: one workgroup
+// at 1-2 waves per SIMD reads a key block's slabs serially (scripts/experiments.md)
 template <typename T, int D>
-__global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(const float* __restrict__ part, int ns, int B, int H, int N,
-                                                            void* out, int64_t sb, int64_t sh, int64_t sn, float scale,
-                                                            const float* rcos, const float* rsin, const int64_t* rpos) {
+__global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(const SplitSum s0, const SplitSum s1, const SplitSum s2, int H) {
   typedef typename Elem<T>::storage S;
   constexpr int Q4 = D / 4;
-  const int64_t rows = (int64_t)B * H * N;
-  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (gid >= rows * Q4) return;
+  int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  SplitSum a = s0;  // (a copy, not a pointer into the kernel arguments: that would go to scratch)
+  if (gid >= s0.units) {
+    gid -= s0.units;
+    a = s1;
+    if (gid >= s1.units) {
+      gid -= s1.units;
+      a = s2;
+      if (gid >= s2.units) return;
+    }
+  }
+  const int64_t rows = a.units / Q4;
   const int64_t row = gid / Q4;
   const int d = 4 * (int)(gid % Q4);
   float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
-  for (int s = 0; s < ns; ++s) {
-    const float4 a = *reinterpret_cast<const float4*>(part + (s * rows + row) * D + d);
-    v0 += a.x; v1 += a.y; v2 += a.z; v3 += a.w;
+  for (int s = 0; s < a.ns; ++s) {
+    const float4 x = *reinterpret_cast<const float4*>(a.part + (s * rows + row) * D + d);
+    v0 += x.x; v1 += x.y; v2 += x.z; v3 += x.w;
   }
-  v0 *= scale; v1 *= scale; v2 *= scale; v3 *= scale;
-  const int bh = (int)(row / N), n = (int)(row % N), b = bh / H, h = bh % H;
-  if (rcos != nullptr) {
-    const Rope rope{rcos, rsin, D / 2};
-    rope_inv4(v0, v1, v2, v3, rope, rpos ? rpos[(int64_t)b * N + n] : n, d);
+  v0 *= a.scale; v1 *= a.scale; v2 *= a.scale; v3 *= a.scale;
+  const int bh = (int)(row / a.N), n = (int)(row % a.N), b = bh / H, h = bh % H;
+  if (a.rcos != nullptr) {
+    const Rope rope{a.rcos, a.rsin, D / 2};
+    rope_inv4(v0, v1, v2, v3, rope, a.rpos ? a.rpos[(int64_t)b * a.N + n] : n, d);
   }
-  store4<T>((S*)out + b * sb + h * sh + (int64_t)n * sn + d, make_float4(v0, v1, v2, v3));
+  store4<T>((S*)a.out + b * a.sb + h * a.sh + (int64_t)n * a.sn + d, make_float4(v0, v1, v2, v3));
 }
 
 // delta = rowsum(dO·O) and lse·log2e of every query row, as the dQ kernel's prologue computes them
@@ -825,22 +848,14 @@ void launch_bwd_v(const AttnBwdParams& bp, hipStream_t s, dim3 gq, dim3 gk, dim3
   hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, C, R, DMA>), gq, block, 0, s, bp);
   hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, C, R, DMA>), gk, block, 0, s, bp);
   const AttnParams& p = bp.f;
+  if (bp.ksplit == 1 && bp.qsplit == 1) return;
   const float* rc = R != 0 ? p.rope_cos : nullptr;
-  if (bp.ksplit > 1) {
-    const int64_t q4 = (int64_t)p.B * p.H * p.Nq * (D / 4);
-    hipLaunchKernelGGL((fa_bwd_reduce_kernel<T, D>), dim3((unsigned)((q4 + 255) / 256)), block, 0, s, bp.dq_part,
-                       bp.ksplit, p.B, p.H, p.Nq, bp.dq, bp.dq_sb, bp.dq_sh, bp.dq_sn, p.scale, rc, p.rope_sin,
-                       p.rope_pos);
-  }
-  if (bp.qsplit > 1) {
-    const int64_t k4 = (int64_t)p.B * p.H * p.Nk * (D / 4);
-    const dim3 g((unsigned)((k4 + 255) / 256));
-    hipLaunchKernelGGL((fa_bwd_reduce_kernel<T, D>), g, block, 0, s, bp.dk_part, bp.qsplit, p.B, p.H, p.Nk, bp.dk,
-                       bp.dk_sb, bp.dk_sh, bp.dk_sn, p.scale, rc, p.rope_sin, p.rope_pos);
-    hipLaunchKernelGGL((fa_bwd_reduce_kernel<T, D>), g, block, 0, s, bp.dv_part, bp.qsplit, p.B, p.H, p.Nk, bp.dv,
-                       bp.dv_sb, bp.dv_sh, bp.dv_sn, 1.f, (const float*)nullptr, (const float*)nullptr,
-                       (const int64_t*)nullptr);
-  }
+  const int64_t q4 = bp.ksplit > 1 ? (int64_t)p.B * p.H * p.Nq * (D / 4) : 0;
+  const int64_t k4 = bp.qsplit > 1 ? (int64_t)p.B * p.H * p.Nk * (D / 4) : 0;
+  const SplitSum sq{bp.dq_part, bp.ksplit, p.Nq, bp.dq, bp.dq_sb, bp.dq_sh, bp.dq_sn, p.scale, rc, p.rope_sin, p.rope_pos, q4};
+  const SplitSum sk{bp.dk_part, bp.qsplit, p.Nk, bp.dk, bp.dk_sb, bp.dk_sh, bp.dk_sn, p.scale, rc, p.rope_sin, p.rope_pos, k4};
+  const SplitSum sv{bp.dv_part, bp.qsplit, p.Nk, bp.dv, bp.dv_sb, bp.dv_sh, bp.dv_sn, 1.f, nullptr, nullptr, nullptr, k4};
+  hipLaunchKernelGGL((fa_bwd_reduce_kernel<T, D>), dim3((unsigned)((q4 + 2 * k4 + 255) / 256)), block, 0, s, sq, sk, sv, p.H);
 }
 
 template <typename T, int D, bool C>

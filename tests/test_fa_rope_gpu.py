@@ -26,9 +26,10 @@ def _ref(q, k, v, cos, sin, pos):
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("with_pos", [False, True])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
-def test_fa_fused_rope(D, with_pos, dt):
+@pytest.mark.parametrize("N", [160, 512])  # 512: the split backward (dQ / dK rotated back by its reducers)
+def test_fa_fused_rope(D, with_pos, dt, N):
     torch.manual_seed(0)
-    B, H, N, ctx = 2, 3, 160, 256
+    B, H, ctx = 2, 3, max(256, N)
     re = RotaryEmbedding(ctx, D, 10000.0).to(DEV)
     cos, sin = re.cos.contiguous(), re.sin.contiguous()
     mk = lambda: torch.randn(B, N, H, D, device=DEV, dtype=dt).transpose(1, 2).requires_grad_(True)

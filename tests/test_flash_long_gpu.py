@@ -164,10 +164,13 @@ def test_split_kv_forward_matches(dt, causal, N, D, monkeypatch):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("N,D", [(2048, 64), (4096, 128), (4096, 32), (1024, 16), (2048, 80)])
+@pytest.mark.parametrize(
+    "N,D", [(2048, 64), (4096, 128), (4096, 32), (1024, 16), (2048, 80), (256, 32), (512, 16), (384, 64), (1000, 64)]
+)
 def test_split_backward_matches(dt, causal, N, D, monkeypatch):
     """B 1, H 1: the two-kernel backward splits the dQ kernel over keys and the dK/dV kernel over
-    queries (fp32 partials + reduce); it must match the unsplit two-kernel form and fp64."""
+    queries (fp32 partials, summed inside the dK/dV kernel: dQ by every workgroup's share, dK/dV by
+    the last split to arrive per key block); it must match the unsplit two-kernel form and fp64."""
     from cs336_systems.ops._ext import ops as hip_ops
 
     if dt == torch.float32 and D in (16, 80):
