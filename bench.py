@@ -150,7 +150,7 @@ def parse(argv=None):
         # 580.8 / 580.9 / 582.6 off (profiles/r5_opt_overlap_ab.md): the HBM-bound update of each
         # layer's weights runs beside the next layers' backward. (Round 1, batch 24 and the older
         # kernels: 193.0 on vs 189.2 off.) Bitwise the same update (tests/test_opt_overlap_gpu.py)
-        help="run the AdamW update during backward on a side stream (auto: on GPU when clip == 0 and not sharded)",
+        help="run the AdamW update during backward on a side stream (auto: on a single GPU when clip == 0 and not sharded)",
     )
     ap.add_argument(
         "--gemm",
@@ -365,8 +365,10 @@ def main(argv=None):
         ddp_model = wrap_ddp(model, args.ddp, bucket_size_mb=bucket, **kw)
     else:
         ddp_model = model
+    # auto: one rank only. Beside RCCL's collectives the update would also compete for the CUs and
+    # HBM the bucket all-reduces use, and that has no measurement yet (--overlap-opt on forces it)
     overlap = args.overlap_opt == "on" or (
-        args.overlap_opt == "auto" and device.type == "cuda" and args.clip == 0 and not args.sharded
+        args.overlap_opt == "auto" and device.type == "cuda" and args.clip == 0 and not args.sharded and world == 1
     )
     if zero:
         opt = ddp_model.optimizer
