@@ -11,6 +11,10 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "cs336/kernels.h"
@@ -744,6 +748,36 @@ at::Tensor xent_bwd(const at::Tensor& gs, const at::Tensor& z, const at::Tensor&
 // ------------------------------------------------------------------------------------------
 // multi-tensor
 // ------------------------------------------------------------------------------------------
+// Device copy of a multi-tensor launch's pointer / size table, reused while the table repeats: the
+// optimizer's parameter, state and shadow pointers are fixed and the caching allocator gives the
+// gradients the same addresses step after step, so steady-state steps issue no host-to-device blit
+// per launch (with the update overlapped with the backward, each blit waited for a CU beside the
+// one-workgroup-per-CU GEMMs: profiles/r5_2p7b_roofline_b32_ovl.md). Keyed by the exact contents,
+// the device and the stream; a copy is only reused on the stream that enqueued it (ordered after
+// the copy), and it stays allocated while cached. Step time: XL 573.6-574.3 -> 574.0-574.5 ms,
+// 2.7b 607.2 / 608.1 -> 606.9 / 605.9 ms (profiles/r5_table_cache_ab.log): within noise, 56-88
+// fewer blit kernels per step.
+at::Tensor device_table(const std::vector<int64_t>& h, c10::Device device) {
+  static std::mutex mu;
+  // leaked on purpose: tensors freed by a static destructor at exit would reach a torn-down allocator
+  static auto& cache = *new std::unordered_map<std::string, at::Tensor>();
+  const hipStream_t st = stream();
+  std::string key(sizeof(st) + sizeof(int) + h.size() * sizeof(int64_t), '\0');
+  const int di = device.index();
+  std::memcpy(&key[0], &st, sizeof(st));
+  std::memcpy(&key[sizeof(st)], &di, sizeof(int));
+  std::memcpy(&key[sizeof(st) + sizeof(int)], h.data(), h.size() * sizeof(int64_t));
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  at::Tensor host = at::empty({(int64_t)h.size()}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+  std::memcpy(host.data_ptr<int64_t>(), h.data(), h.size() * sizeof(int64_t));
+  at::Tensor dev = host.to(device, /*non_blocking=*/true);
+  if (cache.size() >= 4096) cache.clear();  // a workload whose tables never repeat: bounded
+  cache.emplace(std::move(key), dev);
+  return dev;
+}
+
 struct HostTable {
   at::Tensor dev;  // keeps the device copy alive until the ops that use it are enqueued
   cs336::TensorTable tt;
@@ -754,8 +788,8 @@ HostTable build_table(const std::vector<std::vector<at::Tensor>>& lists) {
   const int nptr = (int)lists.size();
   for (const auto& l : lists) TORCH_CHECK((int)l.size() == n, "cs336: tensor lists must have equal length");
   const int64_t len = (int64_t)n * nptr + (n + 1) + n;
-  at::Tensor host = at::empty({len}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
-  int64_t* h = host.data_ptr<int64_t>();
+  std::vector<int64_t> hv((size_t)len);
+  int64_t* h = hv.data();
   int64_t chunks = 0;
   for (int i = 0; i < n; ++i) {
     const at::Tensor& t0 = lists[0][i];
@@ -771,7 +805,7 @@ HostTable build_table(const std::vector<std::vector<at::Tensor>>& lists) {
   }
   h[(int64_t)n * nptr + n] = chunks;
   HostTable ht;
-  ht.dev = host.to(lists[0][0].device(), /*non_blocking=*/true);
+  ht.dev = device_table(hv, lists[0][0].device());
   const int64_t* d = ht.dev.data_ptr<int64_t>();
   ht.tt.ptrs = d;
   ht.tt.chunk_base = d + (int64_t)n * nptr;
@@ -823,8 +857,8 @@ void adamw_step_t(std::vector<at::Tensor> params, std::vector<at::Tensor> grads,
   const at::ScalarType gt = grads[0].scalar_type();
   check_same_dtype(grads, gt, "grads");
   const int64_t len = (int64_t)n * 6 + (n + 1) + (int64_t)n * 3;
-  at::Tensor host = at::empty({len}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
-  int64_t* h = host.data_ptr<int64_t>();
+  std::vector<int64_t> hv((size_t)len);
+  int64_t* h = hv.data();
   int64_t tiles = 0;
   auto aligned = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
   for (int i = 0; i < n; ++i) {
@@ -851,7 +885,7 @@ void adamw_step_t(std::vector<at::Tensor> params, std::vector<at::Tensor> grads,
   }
   h[(int64_t)n * 6 + n] = tiles;
   c10::DeviceGuard guard(params[0].device());
-  at::Tensor dev = host.to(params[0].device(), /*non_blocking=*/true);
+  at::Tensor dev = device_table(hv, params[0].device());
   const int64_t* dptr = dev.data_ptr<int64_t>();
   const double alpha_t = lr * (std::sqrt(1.0 - std::pow(beta2, (double)step)) / (1.0 - std::pow(beta1, (double)step)));
   cs336::adamw_step_t(dptr, dptr + (int64_t)n * 6, dptr + (int64_t)n * 6 + (n + 1), n, tiles, to_dtype(grads[0]),
