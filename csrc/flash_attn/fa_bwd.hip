@@ -95,24 +95,21 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const AttnBwdParams bp) 
       qf[i] = *reinterpret_cast<const uint4*>(Qp + (int64_t)qrow * p.q_sn + e);
       if (ROPE == 1) qf[i] = rope_chunk<T>(qf[i], rope, qpos, e, 1.f);
       dof[i] = *reinterpret_cast<const uint4*>(dOp + (int64_t)qrow * bp.do_sn + e);
-      // delta partial over this lane's half of d (fa_bwd_delta_kernel sums in the same order)
-      if (!bp.delta_ready) {
+      // delta partial over this lane's half of d
 #pragma unroll
-        for (int k = 0; k < EPC; k += 4) {
-          const float4 a = load4<T>(dOp + (int64_t)qrow * bp.do_sn + e + k);
-          const float4 c = load4<T>(Op + (int64_t)qrow * p.o_sn + e + k);
-          delta += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
-        }
+      for (int k = 0; k < EPC; k += 4) {
+        const float4 a = load4<T>(dOp + (int64_t)qrow * bp.do_sn + e + k);
+        const float4 c = load4<T>(Op + (int64_t)qrow * p.o_sn + e + k);
+        delta += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
       }
     } else {
       qf[i] = dof[i] = make_uint4(0, 0, 0, 0);
     }
   }
-  if (bp.delta_ready) delta = valid_q ? -bp.delta[row_lin] : 0.f;
-  else delta += __shfl_xor(delta, 32, 64);
+  delta += __shfl_xor(delta, 32, 64);
   const float lse2 = valid_q ? p.lse[row_lin] * kLog2e : INFINITY;
   // row constants of the dK/dV kernel, pre-transformed so they load straight into its accumulators
-  if (valid_q && hh == 0 && sp == 0 && !bp.delta_ready) {
+  if (valid_q && hh == 0 && sp == 0) {
     bp.delta[row_lin] = -delta;
     bp.lrow[row_lin] = -lse2;
   }
@@ -807,44 +804,10 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(const SplitSum s0, c
   store4<T>((S*)a.out + b * a.sb + h * a.sh + (int64_t)n * a.sn + d, make_float4(v0, v1, v2, v3));
 }
 
-// delta = rowsum(dO·O) and lse·log2e of every query row, as the dQ kernel's prologue computes them
-// (same lane mapping and summation order: bitwise the same values), for the concurrent launch below
-template <typename T, int D>
-__global__ __launch_bounds__(256) void fa_bwd_delta_kernel(const AttnBwdParams bp) {
-  typedef typename Elem<T>::storage S;
-  const AttnParams& p = bp.f;
-  constexpr bool F32 = std::is_same<T, float>::value;
-  constexpr int DP = PadD<D>::value, EPC = 16 / (int)sizeof(S), NQF = F32 ? DP / 8 : DP / 16;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31, hh = lane >> 5;
-  const int64_t r = (int64_t)blockIdx.x * 128 + wave * 32 + l32;  // (b·H + h)·Nq + n
-  const bool valid = r < (int64_t)p.B * p.H * p.Nq;
-  const int64_t bh = valid ? r / p.Nq : 0;
-  const int n = valid ? (int)(r % p.Nq) : 0, b = (int)(bh / p.H), h = (int)(bh % p.H);
-  const S* dOp = (const S*)bp.dout + b * bp.do_sb + h * bp.do_sh + (int64_t)n * bp.do_sn;
-  const S* Op = (const S*)p.o + b * p.o_sb + h * p.o_sh + (int64_t)n * p.o_sn;
-  float delta = 0.f;
-#pragma unroll
-  for (int i = 0; i < NQF; ++i) {
-    const int e = F32 ? (hh * (DP / 2) + 4 * i) : (16 * i + 8 * hh);
-    if (valid && (DP == D || e < D)) {
-#pragma unroll
-      for (int k = 0; k < EPC; k += 4) {
-        const float4 a = load4<T>(dOp + e + k);
-        const float4 c = load4<T>(Op + e + k);
-        delta += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
-      }
-    }
-  }
-  delta += __shfl_xor(delta, 32, 64);
-  if (valid && hh == 0) {
-    bp.delta[r] = -delta;
-    bp.lrow[r] = -(p.lse[r] * kLog2e);
-  }
-}
-
 template <typename T, int D, bool C, int R, bool DMA>
 void launch_bwd_v(const AttnBwdParams& bp, hipStream_t s, dim3 gq, dim3 gk, dim3 block) {
-  // (a two-stream form -- dK/dV beside dQ -- measured slower: profiles/r4_fa_conc.md; retired in round 5)
+  // (a two-stream form -- dK/dV beside dQ after a delta prep kernel -- measured slower:
+  // profiles/r4_fa_conc.md; removed in round 5)
   hipLaunchKernelGGL((fa_bwd_dq_kernel<T, D, C, R, DMA>), gq, block, 0, s, bp);
   hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, D, C, R, DMA>), gk, block, 0, s, bp);
   const AttnParams& p = bp.f;

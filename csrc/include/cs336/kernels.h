@@ -178,9 +178,6 @@ struct AttnBwdParams {
   float* dq_part = nullptr;
   float* dk_part = nullptr;
   float* dv_part = nullptr;
-  // two-kernel form: delta / lrow already written by a prep kernel (the dQ kernel then reads them
-  // instead of computing them, so the dK/dV kernel can run beside it on a second stream)
-  int delta_ready = 0;
 };
 
 void flash_attn_fwd(const AttnParams& p, DType t, hipStream_t s);
