@@ -365,10 +365,11 @@ def main(argv=None):
         ddp_model = wrap_ddp(model, args.ddp, bucket_size_mb=bucket, **kw)
     else:
         ddp_model = model
-    # auto: one rank only. Beside RCCL's collectives the update would also compete for the CUs and
-    # HBM the bucket all-reduces use, and that has no measurement yet (--overlap-opt on forces it)
+    # auto: without a process group only. Beside RCCL's collectives the update also competes for the
+    # CUs and HBM the bucket all-reduces use: unmeasured at N > 1, and under the one-rank DDP wrapper
+    # (--ddp-world1) 608.3 / 609.1 ms on vs 606.6 / 605.5 off (profiles/r5_opt_overlap_ab.md)
     overlap = args.overlap_opt == "on" or (
-        args.overlap_opt == "auto" and device.type == "cuda" and args.clip == 0 and not args.sharded and world == 1
+        args.overlap_opt == "auto" and device.type == "cuda" and args.clip == 0 and not args.sharded and not dist_on
     )
     if zero:
         opt = ddp_model.optimizer
