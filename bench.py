@@ -7,8 +7,10 @@ data-parallel over RCCL/xGMI, tokens/s for the whole node (BASELINE.json metric/
         --master-port 29500 bench.py --gpus 8 --steps 10 --warmup 3
 
 One step = zero grads → forward (bf16 autocast over fp32 master weights; HIP RMSNorm/RoPE/
-FlashAttention-2/SwiGLU kernels, hipBLASLt GEMMs) → fused HIP cross-entropy → backward with the
-bucketed DDP all-reduce overlapped (N > 1) → fused multi-tensor HIP AdamW on all 2.0 B params.
+FlashAttention-2 kernels, cs336 MFMA GEMMs with the SwiGLU / RoPE epilogues fused, per-problem
+table against hipBLASLt) → fused HIP cross-entropy → backward with the bucketed DDP all-reduce
+overlapped (N > 1) → fused multi-tensor HIP AdamW on all 2.0 B params (on one GPU launched chunk
+by chunk during the backward, as gradients become final).
 Model "xl" = d_model 1600, 48 layers, 25 heads (d_head 64), d_ff 6400, vocab 10000, ctx 512
 (reference ``cs336_systems/benchmark.py:247-259``), random init, synthetic tokens.
 Weak scaling: the per-GPU batch is fixed, so global batch = batch * N.
