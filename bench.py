@@ -372,7 +372,7 @@ def main(argv=None):
     # (--ddp-world1) 608.3 / 609.1 ms on vs 606.6 / 605.5 off (profiles/r5_opt_overlap_ab.md)
     overlap = args.overlap_opt == "on" or (
         args.overlap_opt == "auto" and device.type == "cuda" and args.clip == 0 and not args.sharded and not dist_on
-    )
+    ) and not args.graphs  # replayed graphs run no hooks: the optimizer steps eagerly after each replay
     if zero:
         opt = ddp_model.optimizer
         overlap = False

@@ -239,7 +239,9 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def _on_grad_ready(self, p: torch.nn.Parameter) -> None:
         ov = self._ov
-        if ov is None or not ov.active or p.grad is None:
+        # never inside a HIP-graph capture of the backward (utils/graphs.py): the update would be
+        # captured with this step's bias correction and replayed on every later step as well
+        if ov is None or not ov.active or p.grad is None or torch.cuda.is_current_stream_capturing():
             return
         ov.pending.append(p)
         ov.pending_numel += p.numel()
@@ -248,7 +250,7 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def _on_bucket_reduced(self, params, work) -> None:
         ov = self._ov
-        if ov is None or not ov.active:
+        if ov is None or not ov.active or torch.cuda.is_current_stream_capturing():
             return
         ov.pending.extend(p for p in params if p.grad is not None)
         self._flush(work)
