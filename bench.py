@@ -162,7 +162,13 @@ def parse(argv=None):
         # best 331.4/332.2 (the autotuned / cs336 picks win on W1|W3 dX, the o-projection and lm_head)
         help="projection GEMM selection (cs336_systems/ops/gemm.py); sets CS336_GEMM",
     )
-    ap.add_argument("--graphs", action="store_true", help="1 GPU: replay forward+backward from one captured HIP graph")
+    ap.add_argument(
+        "--graphs",
+        default="off",
+        choices=["on", "off"],
+        help="1 GPU: capture the WHOLE step (zero grads, forward, loss, backward, AdamW -- overlapped or not) once "
+        "into a HIP graph and replay it every step (utils/graphs.py GraphedTrainStep; device-side AdamW step counter)",
+    )
     ap.add_argument(
         "--comm-sweep-mb",
         type=float,
@@ -370,9 +376,10 @@ def main(argv=None):
     # auto: without a process group only. Beside RCCL's collectives the update also competes for the
     # CUs and HBM the bucket all-reduces use: unmeasured at N > 1, and under the one-rank DDP wrapper
     # (--ddp-world1) 608.3 / 609.1 ms on vs 606.6 / 605.5 off (profiles/r5_opt_overlap_ab.md)
+    use_graphs = args.graphs == "on" and world == 1 and device.type == "cuda" and not dist_on and args.clip == 0
     overlap = args.overlap_opt == "on" or (
         args.overlap_opt == "auto" and device.type == "cuda" and args.clip == 0 and not args.sharded and not dist_on
-    ) and not args.graphs  # replayed graphs run no hooks: the optimizer steps eagerly after each replay
+    )
     if zero:
         opt = ddp_model.optimizer
         overlap = False
@@ -394,15 +401,17 @@ def main(argv=None):
         # unset grads: the projection GEMMs then write fp32 dW straight into the DDP buckets
         opt.zero_grad(set_to_none=True)
 
+    def eager_step(x, y):
+        """One complete step on the current stream (also what GraphedTrainStep captures)."""
+        zero_grads()
+        with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
+            logits = ddp_model(x)
+            loss = ops.cross_entropy(logits, y)
+        loss.backward()
+        opt.step()
+        return loss
+
     graphed = None
-    if args.graphs and world == 1 and device.type == "cuda":
-        from cs336_systems.utils.graphs import GraphedStep
-
-        def loss_fn(xs, ys):
-            with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
-                return ops.cross_entropy(ddp_model(xs), ys)
-
-        graphed = GraphedStep(loss_fn, model.parameters(), *batches[0])
 
     # exposed communication: GPU time the compute stream spends waiting in
     # finish_gradient_synchronization for collectives that backward did not hide (HIP events)
@@ -411,10 +420,8 @@ def main(argv=None):
 
     def step(i):
         x, y = batches[i % len(batches)]
-        if graphed is not None:  # captured forward + loss + backward, eager AdamW
-            loss = graphed(x, y)
-            opt.step()
-            return loss
+        if graphed is not None:  # the whole captured step, AdamW included
+            return graphed(x, y)
         zero_grads()
         with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
             logits = ddp_model(x)
@@ -451,8 +458,20 @@ def main(argv=None):
     # lt/best GEMM modes time their candidates the first time each problem shape is seen: with
     # --warmup 0 one untimed step still runs so that selection never lands inside the timed region
     n_warm = max(args.warmup, 1) if device.type == "cuda" and args.gemm in ("lt", "best") else args.warmup
+    if use_graphs:
+        # two real steps before the capture: one eager (optimizer state, GEMM selection) and one on the
+        # capture stream inside GraphedTrainStep; the rest of the warmup replays the graph
+        n_warm = max(n_warm, 2)
     for i in range(n_warm):
-        loss = step(i)
+        if use_graphs and i == 1:
+            from cs336_systems.utils.graphs import GraphedTrainStep
+
+            t0 = time.time()
+            graphed = GraphedTrainStep(eager_step, opt, *batches[i % len(batches)], warmup=1)
+            loss = graphed.warmup_loss
+            log(f"captured the whole step into one HIP graph in {time.time() - t0:.1f}s")
+        else:
+            loss = step(i)
         sync()
         log(f"warmup {i}: loss {loss.item():.4f}")
     if device.type == "cuda":
@@ -460,13 +479,19 @@ def main(argv=None):
     barrier()
     sync()
     timing["on"] = True
+    from cs336_systems.utils.gpu_monitor import GpuSampler
+
+    # clock / power / temperature over the timed window (the JSON's gpu_clocks block): explains a
+    # box-to-box spread of the same tree (DVFS under the MFMA-dense step)
+    sampler = GpuSampler(device)
     t_start = time.perf_counter()
     sync_each = os.environ.get("CS336_BENCH_SYNC_EACH", "0") == "1"  # diagnostic: no host run-ahead
-    for i in range(args.steps):
-        loss = step(i)
-        if sync_each:
-            sync()
-    sync()
+    with sampler:
+        for i in range(args.steps):
+            loss = step(i)
+            if sync_each:
+                sync()
+        sync()
     barrier()
     elapsed = time.perf_counter() - t_start
     timing["on"] = False
@@ -526,6 +551,7 @@ def main(argv=None):
         "model_tflops_per_gpu": round(value * flops_tok / world / 1e12, 1),
         "peak_mem_gib": round(peak_gib, 2),
         "final_loss": round(last_loss, 4),
+        "gpu_clocks": sampler.summary(),
     }
     if device.type != "cuda":  # CPU rehearsal: eager PyTorch reference ops, no HIP kernels ran
         out["config"]["optimizer"] = out["config"]["optimizer"].replace("fused HIP AdamW", "PyTorch-reference AdamW")
@@ -545,7 +571,7 @@ def main(argv=None):
                                             and dist.get_backend() == "nccl")
     if world > 1 and run_sweep and not zero:
         # the headline fields are final; free the timed model, then the bounded DDP-variant table
-        del ddp_model, opt, model, batches, graphed
+        del ddp_model, opt, model, batches, graphed, eager_step
         if device.type == "cuda":
             torch.cuda.empty_cache()
         from cs336_systems.bench.ddp import sweep_variants

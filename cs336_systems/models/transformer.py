@@ -84,22 +84,40 @@ class Linear(nn.Module):
 
 
 class _GraphSafeEmbedding(torch.autograd.Function):
-    """Embedding lookup whose backward is one atomic ``index_add_`` into a zeroed table. ATen's
-    embedding backward sorts and partitions the token ids with data-dependent sizes; replaying a
-    HIP graph captured around it faulted in rocprim's partition kernel at the XL shape, so this op
-    is used while a graph is being captured (``utils/graphs.py``)."""
+    """Embedding lookup whose backward does not depend on the token set's size: on GPU the
+    deterministic HIP kernel (``csrc/ops/embedding.hip``: stable sort of the ids, one workgroup per
+    vocabulary row summing its positions' gradient rows in order), else one ``index_add_`` into a
+    zeroed table. ATen's embedding backward sorts and partitions the token ids with data-dependent
+    sizes; replaying a HIP graph captured around it faulted in rocprim's partition kernel at the XL
+    shape. The HIP form is used for every GPU lookup (eager and captured steps then produce the same
+    bits: ``tests/test_graphs_gpu.py``) and writes into the DDP bucket view when there is one
+    (``parallel/ddp.py``: no adopt copy of the 64 MB XL table gradient)."""
 
     @staticmethod
     def forward(ctx, ids, weight):
         ctx.save_for_backward(ids)
         ctx.wshape, ctx.wdtype = weight.shape, weight.dtype
+        ctx.wparam = weight
         return F.embedding(ids, weight)
 
     @staticmethod
     def backward(ctx, g):
         (ids,) = ctx.saved_tensors
-        gw = torch.zeros(ctx.wshape, dtype=torch.float32, device=g.device)
-        gw.index_add_(0, ids.reshape(-1), g.reshape(-1, ctx.wshape[1]).float())
+        V, D = ctx.wshape
+        g2 = g.reshape(-1, D)
+        if D % 4 == 0 and ops.use_hip(g2):
+            if not g2.is_contiguous():
+                g2 = g2.contiguous()
+            sorted_ids, perm = torch.sort(ids.reshape(-1), stable=True)
+            tgt = getattr(ctx.wparam, "_cs336_grad_out", None)
+            if (tgt is not None and ctx.wparam.grad is None and tgt.dtype == torch.float32 and tgt.is_contiguous()
+                    and tuple(tgt.shape) == (V, D)):
+                torch.ops.cs336.embedding_bwd_into(g2, sorted_ids, perm, tgt)
+                return None, tgt.view_as(tgt)  # a fresh alias: adopted as .grad without a copy
+            gw = torch.ops.cs336.embedding_bwd(g2, sorted_ids, perm, V)
+        else:
+            gw = torch.zeros(ctx.wshape, dtype=torch.float32, device=g.device)
+            gw.index_add_(0, ids.reshape(-1), g2.float())
         return None, gw if ctx.wdtype == torch.float32 else gw.to(ctx.wdtype)
 
 
@@ -111,7 +129,8 @@ class Embedding(nn.Module):
         self.weight = nn.Parameter(_trunc_normal((vocab_size, d_model), 1.0, device, dtype), requires_grad=True)
 
     def forward(self, token_ids: torch.Tensor) -> torch.Tensor:
-        if token_ids.is_cuda and not torch.compiler.is_compiling() and torch.cuda.is_current_stream_capturing():
+        if token_ids.is_cuda and not torch.compiler.is_compiling() and (
+                ops.get_backend() != "torch" or torch.cuda.is_current_stream_capturing()):
             return _GraphSafeEmbedding.apply(token_ids, self.weight)
         return F.embedding(token_ids, self.weight)
 

@@ -39,6 +39,27 @@ def _rms_bwd(dy, x, w, rstd):
     return torch.empty_like(x), w.new_empty(w.shape, dtype=torch.float32)
 
 
+@register_fake("cs336::rmsnorm_bwd_into")
+def _rms_bwd_into(dy, x, w, rstd, dw_out):
+    return torch.empty_like(x)
+
+
+@register_fake("cs336::rmsnorm_bwd_add_into")
+def _rms_bwd_add_into(dy, x, w, rstd, dres, emit_bf16, dw_out):
+    return torch.empty_like(x), x.new_empty(x.shape if emit_bf16 else (0,), dtype=torch.bfloat16)
+
+
+@register_fake("cs336::rmsnorm_bwd_add_t_into")
+def _rms_bwd_add_t_into(dy, x, w, rstd, dres, emit_bf16, dw_out):
+    dx2 = x.new_empty(x.shape if emit_bf16 else (0,), dtype=torch.bfloat16)
+    return torch.empty_like(x), dx2, x.new_empty((x.shape[1], x.shape[0]), dtype=torch.bfloat16)
+
+
+@register_fake("cs336::embedding_bwd")
+def _emb_bwd(g, sorted_ids, perm, vocab):
+    return g.new_empty((vocab, g.shape[1]), dtype=torch.float32)
+
+
 @register_fake("cs336::transpose2d")
 def _transpose2d(x):
     return x.new_empty((x.shape[1], x.shape[0]))

@@ -121,8 +121,50 @@ class FusedAdamW(torch.optim.Optimizer):
 
             attach_bf16_shadows([p for g in self.param_groups for p in g["params"]])
         self._ov: _Overlap | None = None
+        # device-resident step counter per param group (enable_device_step): {id(group): (t, alpha)}
+        self._dev_step: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
+        self._dev_step_pending: set[int] = set()
         if overlap_backward:
             self.enable_backward_overlap(ddp=ddp)
+
+    # ------------------------------------------------------------------------------------------
+    # device-side step counter (HIP-graph capture of the whole step)
+    # ------------------------------------------------------------------------------------------
+    def enable_device_step(self) -> None:
+        """Read the bias-corrected step size from device memory instead of a host scalar, so that a
+        HIP graph that captured ``step()`` (``utils/graphs.py`` GraphedTrainStep) replays the correct
+        update on every later step: the first update launch of each step is preceded by one tiny
+        kernel that advances a device step counter and writes ``lr * sqrt(1 - b2^t) / (1 - b1^t)``
+        (double math rounded to fp32, as the host computes it), which the update kernels read. The
+        optimizer state must exist (one eager step) and every parameter of a group must be at the
+        same step. ``lr`` and the betas are read at capture time; the host's per-parameter ``t``
+        follows with :meth:`advance_host_step` after each replay."""
+        for group in self.param_groups:
+            ts = {self.state[p]["t"] for p in group["params"] if "t" in self.state[p]}
+            if not ts:
+                raise RuntimeError("enable_device_step: run one optimizer step first (state is created lazily)")
+            if len(ts) != 1:
+                raise RuntimeError(f"enable_device_step: parameters of a group are at different steps {sorted(ts)}")
+            dev = group["params"][0].device
+            t0 = ts.pop() - 1  # the last completed step; the step kernel advances it before use
+            self._dev_step[id(group)] = (torch.full((1,), t0, dtype=torch.int64, device=dev),
+                                         torch.zeros(1, dtype=torch.float32, device=dev))
+        self._dev_step_pending = set(self._dev_step)
+
+    def advance_host_step(self) -> None:
+        """Host bookkeeping after a replayed captured step: each parameter's ``t`` moves on by one,
+        as an eager step would have moved it (state dicts and checkpoints stay exact)."""
+        for group in self.param_groups:
+            for p in group["params"]:
+                st = self.state.get(p)
+                if st and "t" in st:
+                    st["t"] += 1
+
+    def device_step_value(self) -> int | None:
+        """The device step counter of the first group (tests / checkpoints), or None."""
+        if not self._dev_step:
+            return None
+        return int(next(iter(self._dev_step.values()))[0].item())
 
     # ------------------------------------------------------------------------------------------
     # update launches
@@ -165,10 +207,18 @@ class FusedAdamW(torch.optim.Optimizer):
             t = key[4]
             lr, (beta1, beta2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
             hip = use_hip(ps[0]) and all(x.is_contiguous() for x in ps + gs + ms + vs + ss)
+            alpha = None
+            if id(group) in self._dev_step:
+                if not hip:
+                    raise RuntimeError("enable_device_step needs the HIP update kernels")
+                tdev, alpha = self._dev_step[id(group)]
+                if id(group) in self._dev_step_pending:  # first update launch of this step
+                    ops().adamw_device_step(tdev, alpha, lr, beta1, beta2)
+                    self._dev_step_pending.discard(id(group))
             if hip and wts:
-                ops().adamw_step_t(ps, gs, ms, vs, ss, wts, lr, beta1, beta2, eps, wd, t)
+                ops().adamw_step_t(ps, gs, ms, vs, ss, wts, lr, beta1, beta2, eps, wd, t, alpha)
             elif hip:
-                ops().adamw_step(ps, gs, ms, vs, ss, lr, beta1, beta2, eps, wd, t)
+                ops().adamw_step(ps, gs, ms, vs, ss, lr, beta1, beta2, eps, wd, t, alpha)
             else:
                 for p, g, m, v in zip(ps, gs, ms, vs):
                     adamw_ref_(p, g.to(p.dtype), m, v, lr, beta1, beta2, eps, wd, t)
@@ -196,6 +246,10 @@ class FusedAdamW(torch.optim.Optimizer):
             for p in g["params"]
             if p.grad is not None and (ov is None or id(p) not in ov.stepped)
         ]
+        if items and ov is not None and ov.used and self._dev_step:
+            # the device step kernel of this step ran on the optimizer stream: the updates left for
+            # this stream read its step size
+            torch.cuda.current_stream(ov.stream.device).wait_stream(ov.stream)
         if items:
             self._update(items)
         if ov is not None:
@@ -203,6 +257,7 @@ class FusedAdamW(torch.optim.Optimizer):
             if ov.used:
                 torch.cuda.current_stream(ov.stream.device).wait_stream(ov.stream)
                 ov.used = False
+        self._dev_step_pending = set(self._dev_step)
         return loss
 
     # ------------------------------------------------------------------------------------------
@@ -239,9 +294,10 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def _on_grad_ready(self, p: torch.nn.Parameter) -> None:
         ov = self._ov
-        # never inside a HIP-graph capture of the backward (utils/graphs.py): the update would be
-        # captured with this step's bias correction and replayed on every later step as well
-        if ov is None or not ov.active or p.grad is None or torch.cuda.is_current_stream_capturing():
+        # inside a HIP-graph capture only with the device-side step counter (utils/graphs.py
+        # GraphedTrainStep): otherwise the update would be captured with this step's bias correction
+        # and replayed on every later step as well
+        if ov is None or not ov.active or p.grad is None or (torch.cuda.is_current_stream_capturing() and not self._dev_step):
             return
         ov.pending.append(p)
         ov.pending_numel += p.numel()
@@ -250,7 +306,7 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def _on_bucket_reduced(self, params, work) -> None:
         ov = self._ov
-        if ov is None or not ov.active or torch.cuda.is_current_stream_capturing():
+        if ov is None or not ov.active or (torch.cuda.is_current_stream_capturing() and not self._dev_step):
             return
         ov.pending.extend(p for p in params if p.grad is not None)
         self._flush(work)

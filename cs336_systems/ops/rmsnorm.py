@@ -25,6 +25,17 @@ def rmsnorm_ref(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-5) -> tor
     return (weight * (xf * rms)).to(in_dtype)
 
 
+def _dw_target(weight) -> torch.Tensor | None:
+    """The DDP bucket view to write the weight gradient into (``parallel/ddp.py`` sets
+    ``_cs336_grad_out``), when the gradient is unset and fp32: the column reduction writes it there
+    and autograd adopts an alias of it as ``.grad``, so the bucket needs no copy of it (the GEMMs'
+    dW does the same, ``models/fused.py``)."""
+    t = getattr(weight, "_cs336_grad_out", None)
+    if t is None or weight.grad is not None or t.dtype != torch.float32 or not t.is_contiguous():
+        return None
+    return t if t.shape == weight.shape else None
+
+
 class RMSNormHIP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, eps, out_dtype):
@@ -35,6 +46,7 @@ class RMSNormHIP(torch.autograd.Function):
         y, rstd = ops().rmsnorm_fwd(x2, weight, eps, out_dtype)
         ctx.save_for_backward(x2, weight, rstd)
         ctx.shape = shape
+        ctx.wparam = weight
         return y.view(*shape[:-1], shape[-1])
 
     @staticmethod
@@ -43,6 +55,10 @@ class RMSNormHIP(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
+        tgt = _dw_target(ctx.wparam) if ctx.needs_input_grad[1] else None
+        if tgt is not None:
+            dx = ops().rmsnorm_bwd_into(dy2, x2, weight, rstd, tgt)
+            return dx.view(ctx.shape), tgt.view_as(tgt), None, None
         dx, dw = ops().rmsnorm_bwd(dy2, x2, weight, rstd)
         return dx.view(ctx.shape), dw.to(weight.dtype), None, None
 
@@ -57,6 +73,7 @@ class AddRMSNormHIP(torch.autograd.Function):
         s, y, rstd = ops().add_rmsnorm_fwd(x.reshape(-1, shape[-1]), r.reshape(-1, shape[-1]), weight, eps, out_dtype)
         ctx.save_for_backward(s, weight, rstd)
         ctx.shape, ctx.r_dtype = shape, r.dtype
+        ctx.wparam = weight
         return s.view(shape), y.view(*shape[:-1], y.shape[-1])
 
     @staticmethod
@@ -71,8 +88,13 @@ class AddRMSNormHIP(torch.autograd.Function):
         dy2 = dy.reshape(-1, H)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
+        # dw straight into the DDP bucket view when there is one (no adopt copy)
+        tgt = _dw_target(ctx.wparam) if ctx.needs_input_grad[2] else None
         if ds is None:
-            dx, dw = ops().rmsnorm_bwd(dy2, s, weight, rstd)
+            if tgt is not None:
+                dx, dw = ops().rmsnorm_bwd_into(dy2, s, weight, rstd, tgt), tgt
+            else:
+                dx, dw = ops().rmsnorm_bwd(dy2, s, weight, rstd)
             dr = dx if ctx.r_dtype == dx.dtype else dx.to(ctx.r_dtype)
         else:
             ds2 = ds.reshape(-1, H)
@@ -82,14 +104,23 @@ class AddRMSNormHIP(torch.autograd.Function):
             if emit and _want_transposed_grad(s):
                 # the branch is a narrow projection whose dW takes dYᵀ (models/fused.py): write it
                 # here, transposed through LDS, instead of a separate transpose of dr
-                dx, dx_bf16, dxt, dw = ops().rmsnorm_bwd_add_t(dy2, s, weight, rstd, ds2, True)
+                if tgt is not None:
+                    dx, dx_bf16, dxt = ops().rmsnorm_bwd_add_t_into(dy2, s, weight, rstd, ds2, True, tgt)
+                    dw = tgt
+                else:
+                    dx, dx_bf16, dxt, dw = ops().rmsnorm_bwd_add_t(dy2, s, weight, rstd, ds2, True)
                 from ..models.fused import offer_transposed_grad
 
                 offer_transposed_grad(dx_bf16, dxt)
+            elif tgt is not None:
+                dx, dx_bf16 = ops().rmsnorm_bwd_add_into(dy2, s, weight, rstd, ds2, emit, tgt)
+                dw = tgt
             else:
                 dx, dx_bf16, dw = ops().rmsnorm_bwd_add(dy2, s, weight, rstd, ds2, emit)
             dr = dx_bf16 if emit else (dx if ctx.r_dtype == dx.dtype else dx.to(ctx.r_dtype))
-        return dx.view(ctx.shape), dr.view(ctx.shape), dw.to(weight.dtype), None, None
+        # a fresh alias of the bucket view: AccumulateGrad adopts it as .grad without a copy
+        dw = dw.view_as(dw) if tgt is not None else dw.to(weight.dtype)
+        return dx.view(ctx.shape), dr.view(ctx.shape), dw, None, None
 
 
 # CS336_DYT_FUSED=1: the fused kernel (LDS-staged transposed store) measured 90 us per call vs

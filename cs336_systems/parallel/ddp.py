@@ -105,6 +105,19 @@ def bucket_params(params: list[nn.Parameter], cap_bytes: float) -> list[list[nn.
     return groups
 
 
+class _Done:
+    """The handle of a collective that had nothing to do (world size 1): already complete."""
+
+    def wait(self, timeout=None) -> bool:
+        return True
+
+    def is_completed(self) -> bool:
+        return True
+
+
+_DONE = _Done()
+
+
 class _DDPBase(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, broadcast: bool = True):
         super().__init__()
@@ -120,6 +133,12 @@ class _DDPBase(nn.Module):
         return self.module(*inputs, **kwargs)
 
     def _all_reduce(self, t: torch.Tensor, async_op: bool):
+        if self.world_size == 1:
+            # the mean over one rank is the tensor itself: issue nothing. (RCCL runs ReduceOp.AVG on a
+            # single rank as a separate scaling pass over every bucket -- 11.7 ms/step of XL, a pass that
+            # W > 1 never runs because there the pre-multiply is fused into the ring, so a world-1
+            # measurement of DDP's own cost would be dominated by it: profiles/r5_ddp_sweep_xl_world1.md)
+            return _DONE if async_op else None
         op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
         # Weight gradients may still be in flight on the dW side stream (models/fused.py). Issue
         # the collective from that stream after it has caught up with the main stream: the

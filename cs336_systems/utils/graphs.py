@@ -58,3 +58,57 @@ class GraphedStep:
         for p, g in zip(self.params, self.grads):
             p.grad = g
         return self.loss
+
+
+class GraphedTrainStep:
+    """The WHOLE training step -- zero grads, forward, loss, backward and the optimizer update,
+    including an update overlapped with the backward on a side stream -- captured once into one HIP
+    graph and replayed with one launch per step (the eager step loses ~5 ms of
+    XL step time to launch and host gaps, ``profiles/r5_opt_overlap_ab.md``).
+
+    ``step_fn(x, y) -> loss`` must run one complete eager step on the current stream, starting with
+    ``optimizer.zero_grad(set_to_none=True)`` and ending with ``optimizer.step()``. The constructor
+    runs ``warmup`` such steps on the capture stream (REAL training steps: they update the weights;
+    they also create the optimizer state, which must not be allocated inside the graph), switches
+    the optimizer to its device-side step counter (``FusedAdamW.enable_device_step``: the bias
+    correction is computed on the GPU at every replay) and captures one more step without executing
+    it. Each call copies the batch into the captured input buffers, replays, and advances the
+    optimizer's host-side step counters. Gradients live in the graph's memory pool and are
+    rewritten by every replay; the parameters and optimizer state keep their storage (in-place
+    updates). Hyper-parameters (lr, betas, weight decay) are fixed at capture time.
+    ``tests/test_graphs_gpu.py`` checks a replayed run bitwise against the eager one."""
+
+    def __init__(self, step_fn: Callable[[torch.Tensor, torch.Tensor], torch.Tensor], optimizer, x: torch.Tensor,
+                 y: torch.Tensor, warmup: int = 1):
+        if not x.is_cuda:
+            raise ValueError("GraphedTrainStep captures HIP graphs: inputs must be GPU tensors")
+        if not hasattr(optimizer, "enable_device_step"):
+            raise TypeError("GraphedTrainStep needs an optimizer with a device-side step counter (FusedAdamW)")
+        self.opt = optimizer
+        self.x, self.y = x.clone(), y.clone()
+        dev = x.device
+        self.stream = torch.cuda.Stream(device=dev)
+        self.stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(self.stream):
+            for _ in range(max(1, warmup)):
+                self.warmup_loss = step_fn(self.x, self.y).detach()
+        torch.cuda.current_stream(dev).wait_stream(self.stream)
+        torch.cuda.synchronize(dev)
+        optimizer.enable_device_step()
+        params = [p for g in optimizer.param_groups for p in g["params"]]
+        t_host = [(p, optimizer.state[p]["t"]) for p in params if "t" in optimizer.state[p]]
+        for p in params:  # the eager pool's blocks are not reusable by the graph's private pool
+            p.grad = None
+        torch.cuda.empty_cache()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=self.stream):
+            self.loss = step_fn(self.x, self.y)
+        for p, t in t_host:  # capturing executed nothing: undo the host-side step bookkeeping
+            optimizer.state[p]["t"] = t
+
+    def __call__(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        self.x.copy_(x)
+        self.y.copy_(y)
+        self.graph.replay()
+        self.opt.advance_host_step()
+        return self.loss

@@ -377,21 +377,40 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Te
   return {y, rstd};
 }
 
-std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
-                                               const at::Tensor& rstd) {
+// dw_out: an fp32 (H) contiguous tensor the column reduction writes dw into (a DDP bucket view:
+// parallel/ddp.py), else a fresh tensor
+std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd_impl(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                                    const at::Tensor& rstd, const at::Tensor* dw_out) {
   check_cuda(dy, "dy");
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "cs336: rmsnorm_bwd shapes");
   TORCH_CHECK(x.size(1) % 4 == 0, "cs336: rmsnorm_bwd needs a hidden size divisible by 4");
   c10::DeviceGuard g(x.device());
   at::Tensor dx = at::empty_like(x);
-  if (x.size(0) == 0) return {dx, at::zeros({x.size(1)}, x.options().dtype(at::kFloat))};
-  at::Tensor dw = at::empty({x.size(1)}, x.options().dtype(at::kFloat));
+  at::Tensor dw = dw_out ? *dw_out : at::empty({x.size(1)}, x.options().dtype(at::kFloat));
+  if (x.size(0) == 0) return {dx, dw.zero_()};
   const int rows = cs336::rmsnorm_bwd_workspace_rows(x.size(0), x.size(1));
   at::Tensor ws = at::empty({(int64_t)rows, x.size(1)}, x.options().dtype(at::kFloat));
   cs336::rmsnorm_bwd(dy.data_ptr(), to_dtype(dy), x.data_ptr(), to_dtype(x), w.data_ptr(), to_dtype(w),
                      rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(), ws.data_ptr<float>(), x.size(0),
                      x.size(1), stream());
   return {dx, dw};
+}
+
+void check_dw_out(const at::Tensor& dw, const at::Tensor& x) {
+  TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat && dw.is_contiguous() && dw.numel() == x.size(1) &&
+                  dw.device() == x.device(),
+              "cs336: dw_out must be a contiguous fp32 (H) tensor on the input's device");
+}
+
+std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                               const at::Tensor& rstd) {
+  return rmsnorm_bwd_impl(dy, x, w, rstd, nullptr);
+}
+
+at::Tensor rmsnorm_bwd_into(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd,
+                            at::Tensor& dw_out) {
+  check_dw_out(dw_out, x);
+  return std::get<0>(rmsnorm_bwd_impl(dy, x, w, rstd, &dw_out));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -566,9 +585,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> add_rmsnorm_fwd(const at::Tensor&
 }
 
 // dx = rmsnorm_bwd(dy; s) + dres; dx_bf16 = bf16(dx) when emit_bf16 (else an empty tensor)
-std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add(const at::Tensor& dy, const at::Tensor& x,
-                                                               const at::Tensor& w, const at::Tensor& rstd,
-                                                               const at::Tensor& dres, bool emit_bf16) {
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add_impl(const at::Tensor& dy, const at::Tensor& x,
+                                                                    const at::Tensor& w, const at::Tensor& rstd,
+                                                                    const at::Tensor& dres, bool emit_bf16,
+                                                                    const at::Tensor* dw_out) {
   check_cuda(dy, "dy");
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "cs336: rmsnorm_bwd_add shapes");
   TORCH_CHECK(x.size(1) % 4 == 0, "cs336: rmsnorm_bwd_add needs a hidden size divisible by 4");
@@ -580,8 +600,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add(const at::Tensor&
   c10::DeviceGuard g(x.device());
   at::Tensor dx = at::empty_like(x);
   at::Tensor dx2 = emit_bf16 ? at::empty_like(x, x.options().dtype(at::kBFloat16)) : at::empty({0}, x.options().dtype(at::kBFloat16));
-  if (x.size(0) == 0) return {dx, dx2, at::zeros({x.size(1)}, x.options().dtype(at::kFloat))};
-  at::Tensor dw = at::empty({x.size(1)}, x.options().dtype(at::kFloat));
+  at::Tensor dw = dw_out ? *dw_out : at::empty({x.size(1)}, x.options().dtype(at::kFloat));
+  if (x.size(0) == 0) return {dx, dx2, dw.zero_()};
   const int rows = cs336::rmsnorm_bwd_workspace_rows(x.size(0), x.size(1));
   at::Tensor ws = at::empty({(int64_t)rows, x.size(1)}, x.options().dtype(at::kFloat));
   cs336::rmsnorm_bwd_add(dy.data_ptr(), to_dtype(dy), x.data_ptr(), to_dtype(x), w.data_ptr<float>(),
@@ -590,10 +610,24 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add(const at::Tensor&
   return {dx, dx2, dw};
 }
 
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add(const at::Tensor& dy, const at::Tensor& x,
+                                                               const at::Tensor& w, const at::Tensor& rstd,
+                                                               const at::Tensor& dres, bool emit_bf16) {
+  return rmsnorm_bwd_add_impl(dy, x, w, rstd, dres, emit_bf16, nullptr);
+}
+
+std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd_add_into(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                                        const at::Tensor& rstd, const at::Tensor& dres, bool emit_bf16,
+                                                        at::Tensor& dw_out) {
+  check_dw_out(dw_out, x);
+  auto r = rmsnorm_bwd_add_impl(dy, x, w, rstd, dres, emit_bf16, &dw_out);
+  return {std::get<0>(r), std::get<1>(r)};
+}
+
 // also returns the bf16 result transposed, (H, M) row-major, for the dW = dYᵀ·X GEMMs
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add_t(const at::Tensor& dy, const at::Tensor& x,
-                                                                             const at::Tensor& w, const at::Tensor& rstd,
-                                                                             const at::Tensor& dres, bool emit_bf16) {
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add_t_impl(
+    const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w, const at::Tensor& rstd, const at::Tensor& dres,
+    bool emit_bf16, const at::Tensor* dw_out) {
   check_cuda(dy, "dy");
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes() && x.dim() == 2,
               "cs336: rmsnorm_bwd_add_t shapes");
@@ -610,13 +644,28 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add_t(con
   at::Tensor dx = at::empty_like(x);
   at::Tensor dx2 = emit_bf16 ? at::empty_like(x, x.options().dtype(at::kBFloat16)) : at::empty({0}, x.options().dtype(at::kBFloat16));
   at::Tensor dxt = at::empty({H, M}, x.options().dtype(at::kBFloat16));
-  if (M == 0) return {dx, dx2, dxt, at::zeros({H}, x.options().dtype(at::kFloat))};
-  at::Tensor dw = at::empty({H}, x.options().dtype(at::kFloat));
+  at::Tensor dw = dw_out ? *dw_out : at::empty({H}, x.options().dtype(at::kFloat));
+  if (M == 0) return {dx, dx2, dxt, dw.zero_()};
   at::Tensor ws = at::empty({(int64_t)cs336::rmsnorm_bwd_add_t_workspace_rows(M, H), H}, x.options().dtype(at::kFloat));
   cs336::rmsnorm_bwd_add_t(dy.data_ptr(), to_dtype(dy), x.data_ptr(), to_dtype(x), w.data_ptr<float>(),
                            rstd.data_ptr<float>(), dres.data_ptr(), dx.data_ptr(), emit_bf16 ? dx2.data_ptr() : nullptr,
                            dxt.data_ptr(), dw.data_ptr<float>(), ws.data_ptr<float>(), M, H, stream());
   return {dx, dx2, dxt, dw};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add_t(const at::Tensor& dy, const at::Tensor& x,
+                                                                             const at::Tensor& w, const at::Tensor& rstd,
+                                                                             const at::Tensor& dres, bool emit_bf16) {
+  return rmsnorm_bwd_add_t_impl(dy, x, w, rstd, dres, emit_bf16, nullptr);
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_bwd_add_t_into(const at::Tensor& dy, const at::Tensor& x,
+                                                                      const at::Tensor& w, const at::Tensor& rstd,
+                                                                      const at::Tensor& dres, bool emit_bf16,
+                                                                      at::Tensor& dw_out) {
+  check_dw_out(dw_out, x);
+  auto r = rmsnorm_bwd_add_t_impl(dy, x, w, rstd, dres, emit_bf16, &dw_out);
+  return {std::get<0>(r), std::get<1>(r), std::get<2>(r)};
 }
 
 // ------------------------------------------------------------------------------------------
@@ -757,22 +806,42 @@ at::Tensor xent_bwd(const at::Tensor& gs, const at::Tensor& z, const at::Tensor&
 // the copy), and it stays allocated while cached. Step time: XL 573.6-574.3 -> 574.0-574.5 ms,
 // 2.7b 607.2 / 608.1 -> 606.9 / 605.9 ms (profiles/r5_table_cache_ab.log): within noise, 56-88
 // fewer blit kernels per step.
+// HIP-graph capture: a captured launch bakes the table's device address into the graph, and a
+// table first built inside the capture is filled by a captured copy that re-reads its pinned host
+// buffer at every replay. Tables used by a capture therefore move to a second map that is never
+// evicted, together with the host buffer of one built during the capture.
 at::Tensor device_table(const std::vector<int64_t>& h, c10::Device device) {
   static std::mutex mu;
   // leaked on purpose: tensors freed by a static destructor at exit would reach a torn-down allocator
   static auto& cache = *new std::unordered_map<std::string, at::Tensor>();
+  static auto& captured = *new std::unordered_map<std::string, std::pair<at::Tensor, at::Tensor>>();
   const hipStream_t st = stream();
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  TORCH_CHECK(hipStreamIsCapturing(st, &cs) == hipSuccess, "cs336: hipStreamIsCapturing failed");
+  const bool capturing = cs != hipStreamCaptureStatusNone;
   std::string key(sizeof(st) + sizeof(int) + h.size() * sizeof(int64_t), '\0');
   const int di = device.index();
   std::memcpy(&key[0], &st, sizeof(st));
   std::memcpy(&key[sizeof(st)], &di, sizeof(int));
   std::memcpy(&key[sizeof(st) + sizeof(int)], h.data(), h.size() * sizeof(int64_t));
   std::lock_guard<std::mutex> lock(mu);
+  auto pit = captured.find(key);
+  if (pit != captured.end()) return pit->second.first;
   auto it = cache.find(key);
-  if (it != cache.end()) return it->second;
+  if (it != cache.end()) {
+    if (!capturing) return it->second;
+    at::Tensor dev = it->second;  // filled before the capture: pin it for the graph's lifetime
+    cache.erase(it);
+    captured.emplace(std::move(key), std::make_pair(dev, at::Tensor()));
+    return dev;
+  }
   at::Tensor host = at::empty({(int64_t)h.size()}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
   std::memcpy(host.data_ptr<int64_t>(), h.data(), h.size() * sizeof(int64_t));
   at::Tensor dev = host.to(device, /*non_blocking=*/true);
+  if (capturing) {
+    captured.emplace(std::move(key), std::make_pair(dev, host));
+    return dev;
+  }
   if (cache.size() >= 4096) cache.clear();  // a workload whose tables never repeat: bounded
   cache.emplace(std::move(key), dev);
   return dev;
@@ -819,9 +888,56 @@ void check_same_dtype(const std::vector<at::Tensor>& ts, at::ScalarType st, cons
   for (const auto& t : ts) TORCH_CHECK(t.scalar_type() == st, "cs336: ", name, " dtype mismatch");
 }
 
+// ------------------------------------------------------------------------------------------
+// token embedding backward (deterministic, graph-safe): gw = Σ rows of g per token id
+// ------------------------------------------------------------------------------------------
+void embedding_bwd_into(const at::Tensor& g, const at::Tensor& sorted_ids, const at::Tensor& perm, at::Tensor& out) {
+  check_cuda(g, "g");
+  TORCH_CHECK(g.dim() == 2 && g.is_contiguous() && g.size(1) % 4 == 0, "cs336: embedding_bwd g must be contiguous (T, D), D % 4 == 0");
+  TORCH_CHECK(g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kHalf,
+              "cs336: embedding_bwd g dtype");
+  TORCH_CHECK(sorted_ids.scalar_type() == at::kLong && perm.scalar_type() == at::kLong && sorted_ids.is_contiguous() &&
+                  perm.is_contiguous() && sorted_ids.numel() == g.size(0) && perm.numel() == g.size(0),
+              "cs336: embedding_bwd sorted ids / perm must be contiguous int64 of T entries");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.dim() == 2 && out.is_contiguous() &&
+                  out.size(1) == g.size(1) && out.device() == g.device(),
+              "cs336: embedding_bwd out must be a contiguous fp32 (V, D) tensor");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "cs336: embedding_bwd needs 16-B aligned g / out");
+  c10::DeviceGuard dg(g.device());
+  cs336::embedding_bwd(g.data_ptr(), to_dtype(g), sorted_ids.data_ptr<int64_t>(), perm.data_ptr<int64_t>(),
+                       out.data_ptr<float>(), g.size(0), out.size(0), g.size(1), stream());
+}
+
+at::Tensor embedding_bwd(const at::Tensor& g, const at::Tensor& sorted_ids, const at::Tensor& perm, int64_t vocab) {
+  at::Tensor out = at::empty({vocab, g.size(1)}, g.options().dtype(at::kFloat));
+  embedding_bwd_into(g, sorted_ids, perm, out);
+  return out;
+}
+
+// the device-resident step size of a graph-captured update (adamw_device_step), or null
+const float* alpha_ptr(const std::optional<at::Tensor>& alpha_dev, const at::Tensor& like) {
+  if (!alpha_dev.has_value()) return nullptr;
+  const at::Tensor& a = *alpha_dev;
+  TORCH_CHECK(a.is_cuda() && a.device() == like.device() && a.scalar_type() == at::kFloat && a.numel() == 1,
+              "cs336: alpha_dev must be a one-element fp32 tensor on the parameters' device");
+  return a.data_ptr<float>();
+}
+
+// t += 1; alpha = lr·sqrt(1-b2^t)/(1-b1^t) on the device (the bias correction of a HIP-graph-replayed
+// optimizer step, ops/adamw.py FusedAdamW.enable_device_step)
+void adamw_device_step(at::Tensor& t, at::Tensor& alpha, double lr, double beta1, double beta2) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kLong && t.numel() == 1, "cs336: t must be a one-element int64 GPU tensor");
+  TORCH_CHECK(alpha.is_cuda() && alpha.scalar_type() == at::kFloat && alpha.numel() == 1 && alpha.device() == t.device(),
+              "cs336: alpha must be a one-element fp32 tensor on t's device");
+  c10::DeviceGuard g(t.device());
+  cs336::adamw_device_step(t.data_ptr<int64_t>(), alpha.data_ptr<float>(), lr, beta1, beta2, stream());
+}
+
 void adamw_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> exp_avg,
                 std::vector<at::Tensor> exp_avg_sq, std::vector<at::Tensor> shadows, double lr, double beta1,
-                double beta2, double eps, double weight_decay, int64_t step) {
+                double beta2, double eps, double weight_decay, int64_t step,
+                const std::optional<at::Tensor>& alpha_dev) {
   if (params.empty()) return;
   check_same_dtype(params, at::kFloat, "params (fp32 master weights)");
   check_same_dtype(exp_avg, at::kFloat, "exp_avg");
@@ -836,14 +952,16 @@ void adamw_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, s
   // alpha * (sqrt(1 - b2^t) / (1 - b1^t)) in double, as the reference evaluates it in Python
   const double alpha_t = lr * (std::sqrt(1.0 - std::pow(beta2, (double)step)) / (1.0 - std::pow(beta1, (double)step)));
   cs336::adamw_step(ht.tt, to_dtype(grads[0]), shadow, (float)beta1, (float)beta2, (float)(1.0 - beta1),
-                    (float)(1.0 - beta2), (float)eps, (float)(lr * weight_decay), (float)alpha_t, stream());
+                    (float)(1.0 - beta2), (float)eps, (float)(lr * weight_decay), (float)alpha_t,
+                    alpha_ptr(alpha_dev, params[0]), stream());
 }
 
 // AdamW over 2-D weights that also writes each weight's transposed bf16 shadow (Wᵀ, a (C, R) view
 // with unit column stride whose row stride may exceed R: a column block of a grouped Wᵀ)
 void adamw_step_t(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> exp_avg,
                   std::vector<at::Tensor> exp_avg_sq, std::vector<at::Tensor> shadows, std::vector<at::Tensor> wts,
-                  double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step) {
+                  double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
+                  const std::optional<at::Tensor>& alpha_dev) {
   const int n = (int)params.size();
   if (n == 0) return;
   TORCH_CHECK((int)grads.size() == n && (int)exp_avg.size() == n && (int)exp_avg_sq.size() == n &&
@@ -890,7 +1008,7 @@ void adamw_step_t(std::vector<at::Tensor> params, std::vector<at::Tensor> grads,
   const double alpha_t = lr * (std::sqrt(1.0 - std::pow(beta2, (double)step)) / (1.0 - std::pow(beta1, (double)step)));
   cs336::adamw_step_t(dptr, dptr + (int64_t)n * 6, dptr + (int64_t)n * 6 + (n + 1), n, tiles, to_dtype(grads[0]),
                       (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
-                      (float)(lr * weight_decay), (float)alpha_t, stream());
+                      (float)(lr * weight_decay), (float)alpha_t, alpha_ptr(alpha_dev, params[0]), stream());
 }
 
 void multi_tensor_cast_bf16(std::vector<at::Tensor> src, std::vector<at::Tensor> dst) {
@@ -1020,9 +1138,14 @@ void gemm8(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, int64_t epi,
   TORCH_CHECK(cs336::gemm8::launch(p, (int)epi, (int)fn, stream()), "cs336: gemm8 launch (fn ", fn, ")");
 }
 
-// first-round workgroup stagger of gemm8 per epilogue (csrc/gemm/gemm8.hip, set_stagger)
-bool gemm8_stagger(int64_t epi, int64_t ticks, int64_t groups) {
-  return cs336::gemm8::set_stagger((int)epi, (int)ticks, (int)groups);
+// diagnostic stamp buffer of gemm8 (CS336_G8_STAMP builds, scripts/gemm8_stamps.py): uint64 (blocks, 8)
+// or None = off; returns whether this build writes stamps
+bool gemm8_stamps(const std::optional<at::Tensor>& buf) {
+  if (!buf.has_value()) return cs336::gemm8::set_stamp_buffer(nullptr, 0);
+  const at::Tensor& b = *buf;
+  TORCH_CHECK(b.is_cuda() && b.scalar_type() == at::kLong && b.is_contiguous() && b.dim() == 2 && b.size(1) == 8,
+              "cs336: gemm8 stamp buffer must be a contiguous int64 (blocks, 8) GPU tensor");
+  return cs336::gemm8::set_stamp_buffer(reinterpret_cast<uint64_t*>(b.data_ptr<int64_t>()), b.size(0));
 }
 
 // QKV projection forward with RoPE in the store (gemm8 epi 3): c = a @ b.T with columns < rope_cols
@@ -1159,6 +1282,7 @@ TORCH_LIBRARY(cs336, m) {
       "(Tensor, Tensor, Tensor)");
   m.def("rmsnorm_fwd(Tensor x, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor weight, Tensor rstd) -> (Tensor, Tensor)");
+  m.def("rmsnorm_bwd_into(Tensor dy, Tensor x, Tensor weight, Tensor rstd, Tensor(a!) dw_out) -> Tensor");
   m.def("add_rmsnorm_fwd(Tensor x, Tensor r, Tensor weight, float eps, ScalarType? out_dtype) -> (Tensor, Tensor, Tensor)");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("transpose2d_into(Tensor x, Tensor(a!) out) -> ()");
@@ -1168,6 +1292,8 @@ TORCH_LIBRARY(cs336, m) {
   m.def("gemm_plan(int M, int N, int K, bool fp32_out) -> int[]", &gemm_plan);
   m.def("rmsnorm_bwd_add(Tensor dy, Tensor x, Tensor weight, Tensor rstd, Tensor dres, bool emit_bf16) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd_add_t(Tensor dy, Tensor x, Tensor weight, Tensor rstd, Tensor dres, bool emit_bf16) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("rmsnorm_bwd_add_into(Tensor dy, Tensor x, Tensor weight, Tensor rstd, Tensor dres, bool emit_bf16, Tensor(a!) dw_out) -> (Tensor, Tensor)");
+  m.def("rmsnorm_bwd_add_t_into(Tensor dy, Tensor x, Tensor weight, Tensor rstd, Tensor dres, bool emit_bf16, Tensor(a!) dw_out) -> (Tensor, Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, Tensor? pos, bool inverse) -> Tensor");
   m.def(
       "fa_bwd_into(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, bool causal, float scale, "
@@ -1183,18 +1309,22 @@ TORCH_LIBRARY(cs336, m) {
   m.def("xent_bwd(Tensor g, Tensor logits, Tensor targets, Tensor lse, float mult) -> Tensor");
   m.def(
       "adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, "
-      "Tensor(d!)[] shadows, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
+      "Tensor(d!)[] shadows, float lr, float beta1, float beta2, float eps, float weight_decay, int step, "
+      "Tensor? alpha_dev=None) -> ()");
+  m.def("adamw_device_step(Tensor(a!) t, Tensor(b!) alpha, float lr, float beta1, float beta2) -> ()");
+  m.def("embedding_bwd(Tensor g, Tensor sorted_ids, Tensor perm, int vocab) -> Tensor");
+  m.def("gemm8_stamps(Tensor? buf) -> bool", &gemm8_stamps);
+  m.def("embedding_bwd_into(Tensor g, Tensor sorted_ids, Tensor perm, Tensor(a!) out) -> ()");
   m.def("multi_tensor_l2norm(Tensor[] tensors) -> Tensor");
   m.def("fa_fwd_ot(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor, Tensor)");
   m.def(
       "adamw_step_t(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, "
       "Tensor(d!)[] shadows, Tensor(e!)[] wts, float lr, float beta1, float beta2, float eps, float weight_decay, "
-      "int step) -> ()");
+      "int step, Tensor? alpha_dev=None) -> ()");
   m.def("occupy(int n_workgroups, int lds_bytes, float ms, Tensor(a!) counter) -> ()");
   m.def("cohort(int n_workgroups, int lds_bytes, float deadline_ms, Tensor(a!) state) -> ()");
   m.def("gemm8(Tensor a, Tensor b, Tensor(a!) c, int epi, int fn, Tensor(b!)? h, Tensor? y, int half) -> ()");
   m.def("gemm8_ok(int M, int N, int K, int epi, int half) -> bool", &gemm8_ok);
-  m.def("gemm8_stagger(int epi, int ticks, int groups) -> bool", &gemm8_stagger);
   m.def("gemm8_rope(Tensor a, Tensor b, Tensor(a!) c, Tensor cos, Tensor sin, Tensor? pos, int seq, int rope_cols, int dhead) -> ()");
   m.def("gemm8w(Tensor a, Tensor b, Tensor(a!) out, int splits, bool trans_out, bool accumulate, int fn) -> ()");
   m.def("splitk_sum(Tensor slabs, Tensor(a!) out, bool accumulate) -> ()");
@@ -1207,6 +1337,7 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("fa_bwd", &fa_bwd);
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+  m.impl("rmsnorm_bwd_into", &rmsnorm_bwd_into);
   m.impl("transpose2d", &transpose2d);
   m.impl("transpose2d_into", &transpose2d_into);
   m.impl("gemm", &gemm_new);
@@ -1214,6 +1345,8 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("add_rmsnorm_fwd", &add_rmsnorm_fwd);
   m.impl("rmsnorm_bwd_add", &rmsnorm_bwd_add);
   m.impl("rmsnorm_bwd_add_t", &rmsnorm_bwd_add_t);
+  m.impl("rmsnorm_bwd_add_into", &rmsnorm_bwd_add_into);
+  m.impl("rmsnorm_bwd_add_t_into", &rmsnorm_bwd_add_t_into);
   m.impl("rope", &rope);
   m.impl("fa_bwd_into", &fa_bwd_into);
   m.impl("rope_into", &rope_into);
@@ -1226,6 +1359,9 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("xent_bwd", &xent_bwd);
   m.impl("adamw_step", &adamw_step);
   m.impl("adamw_step_t", &adamw_step_t);
+  m.impl("adamw_device_step", &adamw_device_step);
+  m.impl("embedding_bwd", &embedding_bwd);
+  m.impl("embedding_bwd_into", &embedding_bwd_into);
   m.impl("multi_tensor_l2norm", &multi_tensor_l2norm);
   m.impl("occupy", &occupy);
   m.impl("cohort", &cohort);

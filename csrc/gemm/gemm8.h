@@ -31,15 +31,16 @@ struct Args {
   const float* rsin;
   const int64_t* rpos;
   int rseq, rope_cols, rdh;
-  // first-round stagger (filled by launch() from set_stagger): block b < stg_first of group
-  // g = (b / 8) % stg_groups starts g · stg_ticks (100 MHz ticks) late
-  int stg_first, stg_groups, stg_ticks;
+  // diagnostic builds only (-DCS336_G8_STAMP, scripts/gemm8_stamps.py): per workgroup 8 uint64 --
+  // s_memtime at start / after the prologue / after the main loop / after the epilogue's stores
+  // retired, s_memrealtime at start and end, HW_ID, XCC_ID. Ignored by the shipped build.
+  uint64_t* stamps = nullptr;
 };
 int pick_fn(int N, int epi, int half);
+// diagnostic: later launches with at most `blocks` workgroups write 8 stamps per workgroup into buf
+// (builds with -DCS336_G8_STAMP; returns false in other builds). blocks 0 = off.
+bool set_stamp_buffer(uint64_t* buf, int64_t blocks);
 bool launch(const Args& p, int epi, int fn, hipStream_t s);
-// Stagger of the first round of workgroups for epilogue `epi` (0-3): `groups` groups of CUs, each
-// `ticks` (10 ns) after the previous; ticks 0 = off. Returns false on bad arguments.
-bool set_stagger(int epi, int ticks, int groups);
 
 // Weight gradient with both operands MN-major (csrc/gemm/gemm8w.hip): C[m][n] = Σ_t A[t][m]·B[t][n],
 // A [K][lda] (m < M), B [K][ldb] (n < N), fp32 out. trans_out: C[m][n] stored at c[n·ldc + m].

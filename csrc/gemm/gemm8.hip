@@ -107,20 +107,10 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
-
-  // ---- first-round stagger -------------------------------------------------------------------
-  // One workgroup per CU and equal tiles keep every CU in lockstep: all reach the epilogue together
-  // and its HBM traffic (EPI 1/2: 0.25-0.65 MB per tile) runs as one chip-wide burst while no CU
-  // multiplies. Delaying groups of first-round workgroups (later ones inherit the offset: a CU takes
-  // its next tile when it frees) spreads the bursts over other CUs' main loops.
-  if (p.stg_ticks > 0 && (int)blockIdx.x < p.stg_first) {
-    const int g = (int)(blockIdx.x >> 3) % p.stg_groups;
-    if (g) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      const uint64_t wait = (uint64_t)g * (uint64_t)p.stg_ticks;
-      while (__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(2);
-    }
-  }
+#ifdef CS336_G8_STAMP
+  const uint64_t st_t0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t st_t1 = 0, st_t2 = 0;
+#endif
 
   // ---- tile coordinates -------------------------------------------------------------------
   // EPI 1: N = 2·half, BN/2 units of each half per tile. EPI 0 also takes an N tail (N % BN != 0,
@@ -276,7 +266,10 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
     vmcnt<0>();
   }
   sbarrier();
-  if (wr == 1) sbarrier();  // second wave group one barrier behind (SIMD partner staggering)
+#ifdef CS336_G8_STAMP
+  st_t1 = __builtin_amdgcn_s_memtime();
+#endif
+  if (wr == 1) sbarrier();  // second wave group one barrier behind (SIMD partners offset)
 
   for (int t = 0; t < nkt; ++t) {
     const uint32_t st = (uint32_t)((t & 1) * STAGE);
@@ -326,9 +319,12 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
     mma(4, fa, fb0, 0, FB0);
     sbarrier();
   }
-  if (wr == 0) sbarrier();  // balance the stagger
+  if (wr == 0) sbarrier();  // balance the wave-group offset
   lgkm0();
   sbarrier();
+#ifdef CS336_G8_STAMP
+  st_t2 = __builtin_amdgcn_s_memtime();
+#endif
 
   // ---- epilogue ----------------------------------------------------------------------------
   // cache policy of the epilogue's streams: the SwiGLU outputs (EPI 1 y and h, EPI 2 da|db) and the
@@ -524,34 +520,31 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(const Args p) {
       __builtin_amdgcn_wave_barrier();
     }
   }
-}
-
-// per-epilogue first-round stagger: {ticks, groups}
-struct Stagger {
-  int ticks, groups;
-};
-Stagger g_stagger[4] = {{0, 1}, {0, 1}, {0, 1}, {0, 1}};
-
-int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
+#ifdef CS336_G8_STAMP
+  vmcnt<0>();
+  __syncthreads();
+  if (tid == 0 && p.stamps) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint64_t* o = p.stamps + 8 * (int64_t)blockIdx.x;
+    const uint64_t t3 = __builtin_amdgcn_s_memtime(), r3 = __builtin_amdgcn_s_memrealtime();
+    o[0] = st_t0; o[1] = st_t1; o[2] = st_t2; o[3] = t3; o[4] = st_r0; o[5] = r3; o[6] = hw; o[7] = xcc;
   }
-  return n;
+#endif
 }
+
+uint64_t* g_stamps = nullptr;  // diagnostic stamp buffer (set_stamp_buffer), null in normal runs
+int64_t g_stamp_blocks = 0;
 
 template <int FN, int EPI>
 void launch_t(const Args& p_in, hipStream_t s) {
   Args p = p_in;
-  p.stg_ticks = g_stagger[EPI].ticks;
-  p.stg_groups = g_stagger[EPI].groups;
-  p.stg_first = cu_count();
   constexpr int BN = 64 * FN;
   const int tail = EPI == 0 ? (p.N % BN != 0 ? 1 : 0) | (p.K % BK != 0 ? 2 : 0) : 0;
   const int tiles_n = (tail & 1) ? (p.N + BN - 1) / BN : p.N / BN;
   const dim3 grid((unsigned)((p.M / BM) * tiles_n)), block(NT);
+  if (g_stamps && (int64_t)grid.x <= g_stamp_blocks) p.stamps = g_stamps;
   if constexpr (EPI == 0) {
     if (tail == 1) {
       hipLaunchKernelGGL((gemm8_kernel<FN, 0, 1>), grid, block, 0, s, p);
@@ -571,10 +564,14 @@ void launch_t(const Args& p_in, hipStream_t s) {
 
 }  // namespace
 
-bool set_stagger(int epi, int ticks, int groups) {
-  if (epi < 0 || epi > 3 || ticks < 0 || ticks > 100000 || groups < 1 || groups > 8) return false;
-  g_stagger[epi] = {groups > 1 ? ticks : 0, groups};
+bool set_stamp_buffer(uint64_t* buf, int64_t blocks) {
+  g_stamps = blocks > 0 ? buf : nullptr;
+  g_stamp_blocks = blocks > 0 ? blocks : 0;
+#ifdef CS336_G8_STAMP
   return true;
+#else
+  return false;  // this build writes no stamps
+#endif
 }
 
 // Tile width for an output of N columns (EPI 1: N = 2·half): 320 if it divides, else 256, else 0.
@@ -603,6 +600,15 @@ bool launch(const Args& p, int epi, int fn, hipStream_t s) {
   // one DMA descriptor per operand with 32-bit offsets: both extents below 2 GiB
   const int64_t lim = (int64_t)0x7fffffff - (1 << 20);
   if (((int64_t)(BM - 1) * p.lda + p.K) * 2 >= lim || ((int64_t)(p.N - 1) * p.ldb + p.K) * 2 >= lim) return false;
+  // the EPI 0-2 epilogue streams (C, h, y) go through per-tile buffer descriptors with 32-bit byte
+  // offsets from the tile's first row: one tile's row range must stay below 2 GiB (EPI 3 stores
+  // through 64-bit pointers)
+  if (epi != 3) {
+    const int64_t c_cols = epi == 2 ? (int64_t)p.N + p.half : (int64_t)p.N;  // EPI 2: [da|db]
+    if (((int64_t)(BM - 1) * p.ldc + c_cols) * 2 >= lim) return false;
+    if (epi == 1 && ((int64_t)(BM - 1) * p.ldh + p.half) * 2 >= lim) return false;
+    if (epi == 2 && ((int64_t)(BM - 1) * p.ldy + p.N + p.half) * 2 >= lim) return false;
+  }
 #define CS336_G8(F, E)        \
   do {                        \
     launch_t<F, E>(p, s);     \

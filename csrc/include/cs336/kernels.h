@@ -79,6 +79,12 @@ void silu_mul_fwd(const void* a, const void* b, void* h, DType t, int64_t M, int
 void silu_mul_bwd(const void* dh, const void* a, const void* b, void* da, void* db, DType t, int64_t M, int64_t F,
                   int64_t ld, hipStream_t s);
 
+// ---- token-embedding backward (csrc/ops/embedding.hip) ----
+// gw[v][:] = sum of g[perm[i]][:] over the run of sorted_ids equal to v (in order); gw fp32 (V, D),
+// every row written; g (n_tok, D) row-major; sorted_ids / perm from a stable sort of the ids; D % 4 == 0
+void embedding_bwd(const void* g, DType gt, const int64_t* sorted_ids, const int64_t* perm, float* gw, int64_t n_tok,
+                   int64_t V, int64_t D, hipStream_t s);
+
 // ---- cross entropy (csrc/ops/xent.hip) ----
 void xent_fwd(const void* z, DType t, const int64_t* tgt, float* loss, float* lse, int64_t M, int64_t V,
               hipStream_t s);
@@ -98,14 +104,19 @@ constexpr int64_t kMTChunk = 32768;  // elements per workgroup chunk
 
 // scalars are rounded to fp32 from double exactly like the reference's Python-float * fp32-tensor ops
 // table pointers per tensor: p, g, m, v (+ bf16 shadow when shadow == true)
+// alpha_dev: when non-null, the step size lr·sqrt(1-b2^t)/(1-b1^t) is read from device memory (written
+// by adamw_device_step) instead of alpha_t, so a HIP graph can replay the update on later steps
 void adamw_step(const TensorTable& tt, DType grad_t, bool shadow, float beta1, float beta2, float one_minus_beta1,
-                float one_minus_beta2, float eps, float lr_wd, float alpha_t, hipStream_t s);
+                float one_minus_beta2, float eps, float lr_wd, float alpha_t, const float* alpha_dev, hipStream_t s);
 // 2-D weights, also writing the transposed bf16 shadow: per tensor 6 pointers (p, g, m, v, shadow,
 // Wᵀ at its first element) and dims (R, C, ldt); tiles of 256 rows x 64 columns; R, C multiples of 8,
 // every pointer 16-B aligned, ldt a multiple of 8 (host checks)
 void adamw_step_t(const int64_t* ptrs, const int64_t* tile_base, const int64_t* dims, int n, int64_t total_tiles,
                   DType grad_t, float beta1, float beta2, float one_minus_beta1, float one_minus_beta2, float eps,
-                  float lr_wd, float alpha_t, hipStream_t s);
+                  float lr_wd, float alpha_t, const float* alpha_dev, hipStream_t s);
+// Device-side step counter of a captured optimizer step: t += 1, alpha = lr·sqrt(1-b2^t)/(1-b1^t)
+// (double math, rounded to fp32 as the host computes alpha_t)
+void adamw_device_step(int64_t* t, float* alpha, double lr, double beta1, double beta2, hipStream_t s);
 // table pointers per tensor: fp32 src, bf16 dst
 void multi_tensor_cast_bf16(const TensorTable& tt, hipStream_t s);
 void multi_tensor_sumsq(const TensorTable& tt, DType t, float* partials, hipStream_t s);

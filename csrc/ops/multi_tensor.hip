@@ -41,8 +41,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(const int64_t* __restrict__ 
                                                     const int64_t* __restrict__ chunk_base,
                                                     const int64_t* __restrict__ numel, int n, float b1, float b2,
                                                     float omb1, float omb2, float eps, float lr_wd,
-                                                    float alpha_t) {
+                                                    float alpha_h, const float* __restrict__ alpha_dev) {
   constexpr int NP = SHADOW ? 5 : 4;
+  const float alpha_t = alpha_dev ? *alpha_dev : alpha_h;
   const int64_t chunk = blockIdx.x;
   const int t = find_tensor(chunk_base, n, chunk);
   float* p = reinterpret_cast<float*>(ptrs[NP * t + 0]);
@@ -106,8 +107,10 @@ template <typename TG>
 __global__ __launch_bounds__(256) void adamw_t_kernel(const int64_t* __restrict__ ptrs,
                                                       const int64_t* __restrict__ tile_base,
                                                       const int64_t* __restrict__ dims, int n, float b1, float b2,
-                                                      float omb1, float omb2, float eps, float lr_wd, float alpha_t) {
+                                                      float omb1, float omb2, float eps, float lr_wd, float alpha_h,
+                                                      const float* __restrict__ alpha_dev) {
   const int64_t tile = blockIdx.x;
+  const float alpha_t = alpha_dev ? *alpha_dev : alpha_h;
   const int t = find_tensor(tile_base, n, tile);
   float* p = reinterpret_cast<float*>(ptrs[6 * t + 0]);
   const auto* g = reinterpret_cast<const typename Elem<TG>::storage*>(ptrs[6 * t + 1]);
@@ -223,14 +226,14 @@ __global__ __launch_bounds__(256) void scale_kernel(const int64_t* __restrict__ 
 }  // namespace
 
 void adamw_step(const TensorTable& tt, DType grad_t, bool shadow, float beta1, float beta2, float one_minus_beta1,
-                float one_minus_beta2, float eps, float lr_wd, float alpha_t, hipStream_t s) {
+                float one_minus_beta2, float eps, float lr_wd, float alpha_t, const float* alpha_dev, hipStream_t s) {
   if (tt.total_chunks == 0) return;
   const dim3 grid((unsigned)tt.total_chunks), block(256);
   auto go = [&](auto tg, auto sh) {
     using TG = decltype(tg);
     constexpr bool SH = decltype(sh)::value;
     hipLaunchKernelGGL((adamw_kernel<TG, SH>), grid, block, 0, s, tt.ptrs, tt.chunk_base, tt.numel, tt.n, beta1,
-                       beta2, one_minus_beta1, one_minus_beta2, eps, lr_wd, alpha_t);
+                       beta2, one_minus_beta1, one_minus_beta2, eps, lr_wd, alpha_t, alpha_dev);
   };
   auto by_shadow = [&](auto tg) {
     if (shadow) go(tg, std::true_type{});
@@ -245,19 +248,33 @@ void adamw_step(const TensorTable& tt, DType grad_t, bool shadow, float beta1, f
 
 void adamw_step_t(const int64_t* ptrs, const int64_t* tile_base, const int64_t* dims, int n, int64_t total_tiles,
                   DType grad_t, float beta1, float beta2, float one_minus_beta1, float one_minus_beta2, float eps,
-                  float lr_wd, float alpha_t, hipStream_t s) {
+                  float lr_wd, float alpha_t, const float* alpha_dev, hipStream_t s) {
   if (total_tiles == 0) return;
   const dim3 grid((unsigned)total_tiles), block(256);
   auto go = [&](auto tg) {
     using TG = decltype(tg);
     hipLaunchKernelGGL((adamw_t_kernel<TG>), grid, block, 0, s, ptrs, tile_base, dims, n, beta1, beta2,
-                       one_minus_beta1, one_minus_beta2, eps, lr_wd, alpha_t);
+                       one_minus_beta1, one_minus_beta2, eps, lr_wd, alpha_t, alpha_dev);
   };
   switch (grad_t) {
     case DType::F32: go(float{}); break;
     case DType::BF16: go(BF16{}); break;
     case DType::F16: go(F16{}); break;
   }
+}
+
+// One thread: the step counter of a HIP-graph-captured optimizer step and its bias-corrected step
+// size, in double as the host evaluates it (bindings.cpp adamw_step), rounded once to fp32.
+__global__ __launch_bounds__(64) void adamw_device_step_kernel(int64_t* t, float* alpha, double lr, double b1,
+                                                               double b2) {
+  if (threadIdx.x != 0) return;
+  const int64_t s = *t + 1;
+  *t = s;
+  *alpha = (float)(lr * (sqrt(1.0 - pow(b2, (double)s)) / (1.0 - pow(b1, (double)s))));
+}
+
+void adamw_device_step(int64_t* t, float* alpha, double lr, double beta1, double beta2, hipStream_t s) {
+  hipLaunchKernelGGL(adamw_device_step_kernel, dim3(1), dim3(64), 0, s, t, alpha, lr, beta1, beta2);
 }
 
 // bf16 copy of fp32 tensors (initial sync of the compute-weight shadows)

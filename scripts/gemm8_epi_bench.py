@@ -1,8 +1,8 @@
-"""First-round workgroup stagger of gemm8 (csrc/gemm/gemm8.hip) on the XL step's NT projection GEMMs
-at 49152 tokens: every (ticks, groups) setting on every problem, interleaved rounds in one process,
-random operands.
+"""Time gemm8 (csrc/gemm/gemm8.hip) on the XL step's NT projection problems (epilogues 0-2) at 49152
+tokens, random operands, interleaved rounds in one process; with --check the repeated calls must
+agree bitwise. Used per variant build by scripts/g8_variants.sh (CS336_LIB).
 
-    python scripts/gemm8_stagger.py [--settings 0:1,1100:2,2200:2,1100:4] [--rounds 3] [--reps 10]
+    python scripts/gemm8_epi_bench.py [--rounds 3] [--reps 10] [--only swiglu]
 """
 
 import argparse
@@ -39,18 +39,16 @@ def timeit(fn, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--settings", default="0:1,800:2,1400:2,2200:2,700:4,1100:4")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default=None)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--no-check", action="store_true", help="skip the bitwise check (ablation builds)")
+    ap.add_argument("--no-check", action="store_true", help="skip the bitwise repeat check (ablation builds)")
     args = ap.parse_args()
     from cs336_systems import ops
 
     assert ops.load_ext(), ops.load_error()
     cs = torch.ops.cs336
-    settings = [tuple(int(x) for x in s.split(":")) for s in args.settings.split(",")]
     rows = []
     for name, M, N, K, epi in PROBLEMS:
         if args.only and args.only not in name:
@@ -63,23 +61,19 @@ def main():
         h = torch.empty(M, half, device="cuda", dtype=torch.bfloat16) if epi == 1 else None
         y = ((torch.rand(M, 2 * N, device="cuda", generator=g) * 2 - 1) * 3).bfloat16() if epi == 2 else None
         ref = None
-        times = {s: [] for s in settings}
+        times = []
         for _ in range(args.rounds):
-            for s in settings:
-                assert cs.gemm8_stagger(epi, s[0], s[1])
-                times[s].append(timeit(lambda: cs.gemm8(a, b, c, epi, 0, h, y, half), args.reps))
-                if args.no_check:
-                    pass
-                elif ref is None:
-                    ref = c.clone()
-                else:  # the stagger only delays workgroups: results are bitwise identical
-                    assert torch.equal(ref, c), f"{name}: stagger {s} changed the result"
-        cs.gemm8_stagger(epi, 0, 1)
+            times.append(timeit(lambda: cs.gemm8(a, b, c, epi, 0, h, y, half), args.reps))
+            if args.no_check:
+                pass
+            elif ref is None:
+                ref = c.clone()
+            else:  # repeated launches are deterministic
+                assert torch.equal(ref, c), f"{name}: result changed between calls"
         flop = 2.0 * M * N * K
-        row = {"problem": name, "M": M, "N": N, "K": K, "epi": epi}
-        for s, v in times.items():
-            ms = statistics.median(v)
-            row[f"{s[0]}:{s[1]}"] = {"ms": round(ms, 4), "min_ms": round(min(v), 4), "tflops": round(flop / ms / 1e9, 1)}
+        ms = statistics.median(times)
+        row = {"problem": name, "M": M, "N": N, "K": K, "epi": epi,
+               "ms": round(ms, 4), "min_ms": round(min(times), 4), "tflops": round(flop / ms / 1e9, 1)}
         rows.append(row)
         print(json.dumps(row), flush=True)
         del a, b, c, h, y, ref

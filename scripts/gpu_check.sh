@@ -36,6 +36,15 @@ for r in json.load(open('gpurun_out/flash4096.json')):
     rehearse)
       timeout -k 10 300 bash scripts/rehearse_multirank.sh > gpurun_out/rehearse.log 2>&1 || { tail -30 gpurun_out/rehearse.log; exit 1; }
       grep '"metric"' gpurun_out/rehearse.log | cut -c1-300 ;;
+    quick)  # QUICK_TESTS="tests/a.py tests/b.py": a targeted subset of the GPU suite
+      timeout -k 10 600 python -u -m pytest ${QUICK_TESTS:-tests/test_train_graph_gpu.py} -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_quick.log 2>&1 || { tail -60 gpurun_out/gpu_quick.log; exit 1; }
+      tail -3 gpurun_out/gpu_quick.log ;;
+    stamps)  # in-kernel gemm8 phase stamps (CS336_G8_STAMP variant build)
+      CS336_LIB=cs336_systems/_native/variants/stamp/libcs336_hip.so timeout -k 10 300 python -u scripts/gemm8_stamps.py --json gpurun_out/gemm8_stamps.json > gpurun_out/gemm8_stamps.log 2>&1 || { tail -30 gpurun_out/gemm8_stamps.log; exit 1; }
+      cat gpurun_out/gemm8_stamps.log ;;
+    graphab)  # eager step vs the whole step captured in one HIP graph, same box
+      timeout -k 10 900 python scripts/ab.py bench "eager:" "graphs::--graphs on" --rounds ${AB_ROUNDS:-2} --steps 10 --timeout 300 > gpurun_out/graphab.log 2>&1 || { tail -30 gpurun_out/graphab.log; exit 1; }
+      tail -8 gpurun_out/graphab.log ;;
     *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done

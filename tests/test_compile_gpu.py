@@ -1,7 +1,7 @@
 """torch.compile of the Transformer on the HIP path (models/compiled.py custom ops): no graph break
 for the XL and 2.7b models under bf16 autocast, and a compiled train step (inductor) that matches the
-eager step -- loss, gradients, and the parameters after fused-AdamW steps (which also exercises the
-bf16 / Wᵀ weight shadows the custom ops read)."""
+eager step -- loss, gradients, and the parameters after fused-AdamW steps, with and without the bf16 /
+Wᵀ weight shadows that the fused AdamW writes and the custom ops read."""
 
 import pytest
 import torch
@@ -45,13 +45,15 @@ def _small(dev):
                                device=dev)
 
 
-def test_compiled_steps_match_eager():
+@pytest.mark.parametrize("shadows", [False, True])
+def test_compiled_steps_match_eager(shadows):
     _ext()
     torch._dynamo.reset()
     dev = torch.device("cuda", 0)
     mc, me = _small(dev), _small(dev)
     me.load_state_dict(mc.state_dict())
     kw = dict(lr=1e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01)
+    kw["bf16_shadows"] = shadows
     oc, oe = ops.FusedAdamW(mc.parameters(), **kw), ops.FusedAdamW(me.parameters(), **kw)
     x = torch.randint(0, 10000, (2, 256), device=dev)
 

@@ -169,8 +169,8 @@ def test_split_kv_forward_matches(dt, causal, N, D, monkeypatch):
 )
 def test_split_backward_matches(dt, causal, N, D, monkeypatch):
     """B 1, H 1: the two-kernel backward splits the dQ kernel over keys and the dK/dV kernel over
-    queries (fp32 partials, summed inside the dK/dV kernel: dQ by every workgroup's share, dK/dV by
-    the last split to arrive per key block); it must match the unsplit two-kernel form and fp64."""
+    queries into fp32 partial slabs, which ONE reduce launch (fa_bwd_reduce_kernel over SplitSum
+    descriptors) sums for dQ, dK and dV; it must match the unsplit two-kernel form and fp64."""
     from cs336_systems.ops._ext import ops as hip_ops
 
     if dt == torch.float32 and D in (16, 80):

@@ -53,3 +53,36 @@ def test_other_stream_and_reused_memory():
     scale = torch.tensor([0.5], device=DEV)
     hip.multi_tensor_scale_(new, scale)
     assert all(torch.all(t == 1.0).item() for t in new)
+
+
+@pytest.mark.parametrize("cached_first", [False, True])
+def test_captured_launch_keeps_its_table(cached_first):
+    """A multi-tensor launch captured in a HIP graph bakes in the table's device address: the table
+    must stay valid (and hold the same contents) on every replay, whether it was first built inside
+    the capture (its copy node re-reads the host buffer) or taken from the cache built before it, and
+    no later eviction may free it (more distinct tables than the cache bound are built in between)."""
+    hip = _hip()
+    ts = [torch.randn(n, device=DEV) for n in (5000, 64, 777)]
+    if cached_first:
+        hip.multi_tensor_l2norm(ts)
+        torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        hip.multi_tensor_l2norm(ts)  # warm the capturing stream's table
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        out = hip.multi_tensor_l2norm(ts)
+    # churn the evictable cache past its bound with tables that never repeat
+    junk = [torch.zeros(64, device=DEV) for _ in range(4200)]  # held: every table names new addresses
+    for t in junk:
+        hip.multi_tensor_l2norm([t])
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for t in ts:
+            t.normal_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert out.item() == pytest.approx(_ref_norm(ts), rel=1e-5)
