@@ -409,7 +409,9 @@ def main(argv=None):
             loss = ops.cross_entropy(logits, y)
         loss.backward()
         opt.step()
-        return loss
+        # detached: a loss that keeps its autograd graph alive also keeps the parameters' AccumulateGrad
+        # nodes (bound to the stream of their first backward), which breaks a later capture on a side stream
+        return loss.detach()
 
     graphed = None
 
@@ -445,7 +447,7 @@ def main(argv=None):
         elif args.clip > 0:
             ops.clip_grad_norm_(model.parameters(), args.clip)
         opt.step()
-        return loss
+        return loss.detach()
 
     def sync():
         if device.type == "cuda":

@@ -807,14 +807,38 @@ at::Tensor xent_bwd(const at::Tensor& gs, const at::Tensor& z, const at::Tensor&
 // 2.7b 607.2 / 608.1 -> 606.9 / 605.9 ms (profiles/r5_table_cache_ab.log): within noise, 56-88
 // fewer blit kernels per step.
 // HIP-graph capture: a captured launch bakes the table's device address into the graph, and a
-// table first built inside the capture is filled by a captured copy that re-reads its pinned host
-// buffer at every replay. Tables used by a capture therefore move to a second map that is never
-// evicted, together with the host buffer of one built during the capture.
+// table first built inside the capture is filled by a captured copy that re-reads its host bytes at
+// every replay. Tables used by a capture therefore move to a second map that is never evicted, and
+// the host bytes of one built during the capture live in a pinned arena of this file's own
+// (hipHostMalloc'd outside any capture, never freed): PyTorch's caching host allocator cannot serve
+// there (it queries the events of its freed blocks, and one recorded in the capturing stream fails).
+struct CaptureArena {
+  char* base = nullptr;
+  size_t used = 0, cap = 0;
+  void reserve() {  // outside a capture: a fresh 4 MiB block once the current one is 3/4 used
+    if (base && used + (cap >> 2) <= cap) return;
+    void* p = nullptr;
+    TORCH_CHECK(hipHostMalloc(&p, 4u << 20, hipHostMallocDefault) == hipSuccess, "cs336: hipHostMalloc (table arena)");
+    base = static_cast<char*>(p);  // the previous block stays allocated: captured copies read it
+    used = 0;
+    cap = 4u << 20;
+  }
+  const void* put(const std::vector<int64_t>& h) {
+    const size_t bytes = (h.size() * sizeof(int64_t) + 255) & ~(size_t)255;
+    TORCH_CHECK(base && used + bytes <= cap, "cs336: table arena exhausted inside a HIP-graph capture");
+    char* dst = base + used;
+    std::memcpy(dst, h.data(), h.size() * sizeof(int64_t));
+    used += bytes;
+    return dst;
+  }
+};
+
 at::Tensor device_table(const std::vector<int64_t>& h, c10::Device device) {
   static std::mutex mu;
   // leaked on purpose: tensors freed by a static destructor at exit would reach a torn-down allocator
   static auto& cache = *new std::unordered_map<std::string, at::Tensor>();
-  static auto& captured = *new std::unordered_map<std::string, std::pair<at::Tensor, at::Tensor>>();
+  static auto& captured = *new std::unordered_map<std::string, at::Tensor>();
+  static auto& arena = *new CaptureArena();
   const hipStream_t st = stream();
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   TORCH_CHECK(hipStreamIsCapturing(st, &cs) == hipSuccess, "cs336: hipStreamIsCapturing failed");
@@ -826,22 +850,27 @@ at::Tensor device_table(const std::vector<int64_t>& h, c10::Device device) {
   std::memcpy(&key[sizeof(st) + sizeof(int)], h.data(), h.size() * sizeof(int64_t));
   std::lock_guard<std::mutex> lock(mu);
   auto pit = captured.find(key);
-  if (pit != captured.end()) return pit->second.first;
+  if (pit != captured.end()) return pit->second;
   auto it = cache.find(key);
   if (it != cache.end()) {
     if (!capturing) return it->second;
     at::Tensor dev = it->second;  // filled before the capture: pin it for the graph's lifetime
     cache.erase(it);
-    captured.emplace(std::move(key), std::make_pair(dev, at::Tensor()));
+    captured.emplace(std::move(key), dev);
     return dev;
   }
+  if (capturing) {
+    const void* src = arena.put(h);
+    at::Tensor dev = at::empty({(int64_t)h.size()}, at::TensorOptions().dtype(at::kLong).device(device));
+    TORCH_CHECK(hipMemcpyAsync(dev.data_ptr(), src, h.size() * sizeof(int64_t), hipMemcpyHostToDevice, st) == hipSuccess,
+                "cs336: captured table copy");
+    captured.emplace(std::move(key), dev);
+    return dev;
+  }
+  arena.reserve();  // ready before any capture starts
   at::Tensor host = at::empty({(int64_t)h.size()}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
   std::memcpy(host.data_ptr<int64_t>(), h.data(), h.size() * sizeof(int64_t));
   at::Tensor dev = host.to(device, /*non_blocking=*/true);
-  if (capturing) {
-    captured.emplace(std::move(key), std::make_pair(dev, host));
-    return dev;
-  }
   if (cache.size() >= 4096) cache.clear();  // a workload whose tables never repeat: bounded
   cache.emplace(std::move(key), dev);
   return dev;

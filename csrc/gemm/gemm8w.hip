@@ -18,7 +18,10 @@
 // * a K-tile runs as 4 phases split along K -- (k 0-31, rows 0-63), (k 0-31, rows 64-127),
 //   (k 32-63, rows 0-63), (k 32-63, rows 64-127) -- because a DMA granule holds whole t-rows: the
 //   t-rows 0-31 of a stage are free after phase 2 and restaged with the K-tile after next there, the
-//   t-rows 32-63 at the next K-tile's phase 1;
+//   t-rows 32-63 at the next K-tile's phase 1; each half is waited for (counted vmcnt) only one phase
+//   before its first read -- the first half at phase 3 of the previous K-tile, the second half at
+//   phase 1 of its own -- so both have five phases in flight (the round-5 form retired the whole
+//   next K-tile at phase 3: its second half had three);
 // * fp32 accumulators leave straight from registers, 16 B per lane (4 consecutive output columns, or
 //   4 consecutive output rows when the result is stored transposed), into the DDP bucket or a
 //   split-K slab; rows beyond M (the last, padded row tile) are computed and dropped.
@@ -160,8 +163,10 @@ __global__ __launch_bounds__(NT, 2) void gemm8w_kernel(const WArgs p) {
     _Pragma("unroll") for (int i_ = 0; i_ < G::GB_HI; ++i_) if (i_ < nb_)                                  \
       glds(rb, vb[H][i_], sob_, base_ + lb[H][i_]); \
   } while (0)
-  // outstanding DMA of one K-half issue (this wave): the counted wait of phase 3
+  // outstanding DMA of one K-half issue (this wave): n0 = GA + nb_h0, n1 = GA + nb_h1 (n0 + n1 does
+  // not depend on the wave)
   const bool big0 = G::GB_HI != G::GB_LO && wr == 0;  // this wave issues 3 B granules in half 0
+  constexpr int N01 = 2 * G::GA + G::GB_HI + G::GB_LO;  // both halves of one K-tile
 
   // ---- transposed fragment reads ------------------------------------------------------------
   const int g4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
@@ -202,16 +207,17 @@ __global__ __launch_bounds__(NT, 2) void gemm8w_kernel(const WArgs p) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // ---- prologue: K-tile 0 whole, K-tile 1's first half ----------------------------------------
+  // ---- prologue: K-tile 0 whole, K-tile 1's first half; only K-tile 0's first half is waited
+  // for here (its second half at phase 1) ---------------------------------------------------------
   if (nkt > 0) {
     CS336_G8W_ISSUE(0, 0, 0);
     CS336_G8W_ISSUE(1, 0, 0);
     if (nkt > 1) {
       CS336_G8W_ISSUE(0, 1, 1);
-      if (big0) vmcnt<G::GA + G::GB_HI>();
-      else vmcnt<G::GA + G::GB_LO>();
+      vmcnt<N01>();  // younger: K-tile 0's second half, K-tile 1's first half
     } else {
-      vmcnt<0>();
+      if (big0) vmcnt<G::GA + G::GB_LO>();  // younger: K-tile 0's second half (n1)
+      else vmcnt<G::GA + G::GB_HI>();
     }
   }
   sbarrier();
@@ -229,9 +235,12 @@ __global__ __launch_bounds__(NT, 2) void gemm8w_kernel(const WArgs p) {
     sbarrier();
     mma(0);
     sbarrier();
-    // P1: k 0-31, rows 64-127
+    // P1: k 0-31, rows 64-127; retire this K-tile's second half (read from P2 on): issued at the
+    // previous K-tile's P0, it has had five phases in flight
 #pragma unroll
     for (int i = 0; i < 4; ++i) fa[i] = frag(st, SA, arow + 64 + 16 * i, 0);
+    if (t + 1 < nkt) vmcnt<N01>();  // younger: K-tile t+1's two halves
+    else vmcnt<0>();
     wait_a();
     sbarrier();
     mma(4);
@@ -246,15 +255,17 @@ __global__ __launch_bounds__(NT, 2) void gemm8w_kernel(const WArgs p) {
     sbarrier();
     mma(0);
     sbarrier();
-    // P3: k 32-63, rows 64-127; retire K-tile t+1 (only K-tile t+2's first half may stay in flight)
+    // P3: k 32-63, rows 64-127; retire K-tile t+1's first half (read at its P0); its second half and
+    // K-tile t+2's first half stay in flight
 #pragma unroll
     for (int i = 0; i < 4; ++i) fa[i] = frag(st, SA, arow + 64 + 16 * i, 1);
     if (t + 1 < nkt) {
       if (t + 2 < nkt) {
-        if (big0) vmcnt<G::GA + G::GB_HI>();
-        else vmcnt<G::GA + G::GB_LO>();
+        vmcnt<N01>();  // younger: K-tile t+1's second half (P0), K-tile t+2's first half (P2)
+      } else if (big0) {
+        vmcnt<G::GA + G::GB_LO>();  // younger: K-tile t+1's second half (n1)
       } else {
-        vmcnt<0>();
+        vmcnt<G::GA + G::GB_HI>();
       }
     }
     wait_a();

@@ -43,8 +43,16 @@ for r in json.load(open('gpurun_out/flash4096.json')):
       CS336_LIB=cs336_systems/_native/variants/stamp/libcs336_hip.so timeout -k 10 300 python -u scripts/gemm8_stamps.py --json gpurun_out/gemm8_stamps.json > gpurun_out/gemm8_stamps.log 2>&1 || { tail -30 gpurun_out/gemm8_stamps.log; exit 1; }
       cat gpurun_out/gemm8_stamps.log ;;
     graphab)  # eager step vs the whole step captured in one HIP graph, same box
-      timeout -k 10 900 python scripts/ab.py bench "eager:" "graphs::--graphs on" --rounds ${AB_ROUNDS:-2} --steps 10 --timeout 300 > gpurun_out/graphab.log 2>&1 || { tail -30 gpurun_out/graphab.log; exit 1; }
+      timeout -k 10 900 python scripts/ab.py bench "eager:" "graphs:PYTHONFAULTHANDLER=1:--graphs on" --rounds ${AB_ROUNDS:-2} --steps 10 --timeout 300 > gpurun_out/graphab.log 2>&1 || { tail -30 gpurun_out/graphab.log; exit 1; }
       tail -8 gpurun_out/graphab.log ;;
+    dwab)  # weight-gradient GEMMs as the step runs them: base variant lib vs this tree's lib, interleaved
+      for r in 1 2; do
+        for v in base new; do
+          lib=cs336_systems/_native/libcs336_hip.so; [ $v = base ] && lib=cs336_systems/_native/variants/base/libcs336_hip.so
+          CS336_LIB=$lib timeout -k 10 240 python -u scripts/dw_time.py --tag "$v$r" >> gpurun_out/dwab.log 2>&1 || { tail -20 gpurun_out/dwab.log; exit 1; }
+        done
+      done
+      grep '^{' gpurun_out/dwab.log ;;
     *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done
