@@ -348,6 +348,12 @@ def main(argv=None):
         device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
         if device.type == "cuda":
             torch.cuda.set_device(device)
+            # the host threads on the CPUs local to the GPU, as every rank of a multi-GPU run is
+            # (setup_distributed): the eager step's launch stream runs from them
+            # (neutral on one GPU, 585.8-586.0 vs 586.0-586.4 ms: profiles/r6_ddp_world1.md)
+            from cs336_systems.parallel.affinity import pin_rank_to_gpu
+
+            pin_rank_to_gpu(device)
     tmode = None
     if device.type == "cuda":
         assert ops.ext_available(), ops.load_error()
@@ -374,8 +380,10 @@ def main(argv=None):
     else:
         ddp_model = model
     # auto: without a process group only. Beside RCCL's collectives the update also competes for the
-    # CUs and HBM the bucket all-reduces use: unmeasured at N > 1, and under the one-rank DDP wrapper
-    # (--ddp-world1) 608.3 / 609.1 ms on vs 606.6 / 605.5 off (profiles/r5_opt_overlap_ab.md)
+    # CUs and HBM the bucket all-reduces use: with the W = 8 ring's bytes emulated beside the real XL
+    # backward the overlapped update is slower in five of six bucket / channel configurations (+5.6 to
+    # +63.5 ms; 128 MB, 32 channels: 635.0 vs 629.4 ms, profiles/r6_comm_emulation.md), and under the
+    # one-rank DDP wrapper 608.3 / 609.1 ms on vs 606.6 / 605.5 off (profiles/r5_opt_overlap_ab.md)
     use_graphs = args.graphs == "on" and world == 1 and device.type == "cuda" and not dist_on and args.clip == 0
     overlap = args.overlap_opt == "on" or (
         args.overlap_opt == "auto" and device.type == "cuda" and args.clip == 0 and not args.sharded and not dist_on
@@ -486,6 +494,7 @@ def main(argv=None):
     # clock / power / temperature over the timed window (the JSON's gpu_clocks block): explains a
     # box-to-box spread of the same tree (DVFS under the MFMA-dense step)
     sampler = GpuSampler(device)
+    ms0 = torch.cuda.memory_stats(device) if device.type == "cuda" else {}
     t_start = time.perf_counter()
     sync_each = os.environ.get("CS336_BENCH_SYNC_EACH", "0") == "1"  # diagnostic: no host run-ahead
     with sampler:
@@ -514,6 +523,8 @@ def main(argv=None):
             f"allocator: reserved peak {ms.get('reserved_bytes.all.peak', 0) / 2**30:.1f} GiB, "
             f"alloc retries {ms.get('num_alloc_retries', 0)}, device mallocs {ms.get('num_device_alloc', 0)}"
         )
+        alloc_timed = {k: ms.get(k, 0) - ms0.get(k, 0) for k in
+                       ("num_device_alloc", "num_device_free", "num_sync_all_streams", "num_alloc_retries")}
 
     ms_per_step = 1e3 * elapsed / max(args.steps, 1)
     tokens_per_step = args.batch * args.ctx * world
@@ -555,6 +566,12 @@ def main(argv=None):
         "final_loss": round(last_loss, 4),
         "gpu_clocks": sampler.summary(),
     }
+    if device.type == "cuda":  # caching-allocator events inside the timed steps (hipMalloc/hipFree sync)
+        out["allocator_timed"] = alloc_timed
+    if device.type == "cuda" and not dist_on:
+        from cs336_systems.parallel.affinity import affinity_info
+
+        out["cpu_affinity"] = affinity_info()
     if device.type != "cuda":  # CPU rehearsal: eager PyTorch reference ops, no HIP kernels ran
         out["config"]["optimizer"] = out["config"]["optimizer"].replace("fused HIP AdamW", "PyTorch-reference AdamW")
         out["config"]["attention"] = "PyTorch-reference attention (causal)"

@@ -40,7 +40,13 @@ MI355X/RCCL design notes:
   RCCL-shaped occupants (16 or 32 channel blocks) held for each bucket's W = 8 ring time beside the
   real XL backward hide all 48 ms/step of communication at 128 MB (598.8 / 599.2 ms/step against
   599.7 for world-1 DDP), 512 MB exposes the last bucket (+4-8 ms), 32 MB with 32 channels loses
-  52 ms.
+  52 ms. Round 6 re-ran it at the bench's batch 102 with occupants that also MOVE the ring's per-rank
+  HBM bytes (``profiles/r6_comm_emulation.md``): 10.7-20.7 ms/step over world 1 at 32-128 MB, 512 MB
+  +47-78 ms, and the backward-overlapped optimizer update slower beside the collectives in five of six
+  configurations (so ``bench.py`` leaves it off at N > 1).
+* World size 1 issues no collective at all (``_all_reduce``): RCCL runs ``ReduceOp.AVG`` on one rank
+  as a separate scaling pass over every bucket (11.7 ms/step at XL), which no W > 1 ring runs. With it
+  gone the one-rank wrapper is within 1 ms of the plain step (``profiles/r6_ddp_world1.md``).
 * Unlike the reference, buckets hold only ``requires_grad`` parameters (no empty bucket 0, frozen
   params never block a flush).
 * Collective order is identical on every rank: buckets are issued strictly in index order (a

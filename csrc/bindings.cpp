@@ -1084,6 +1084,22 @@ void occupy(int64_t n_workgroups, int64_t lds_bytes, double ms, at::Tensor& coun
   cs336::occupy((int)n_workgroups, (int)lds_bytes, ms, counter.data_ptr<int>(), stream());
 }
 
+// byte-moving occupant (csrc/ops/occupy.hip): src read / dst written, same byte size, 16 KiB multiples
+void occupy_bytes(int64_t n_workgroups, int64_t lds_bytes, double ms, const at::Tensor& src, at::Tensor& dst,
+                  int64_t total_bytes, at::Tensor& counter) {
+  check_cuda(src, "src");
+  TORCH_CHECK(counter.scalar_type() == at::kInt && counter.numel() >= 1, "cs336: occupy counter must be int32");
+  const int64_t nb = src.numel() * src.element_size();
+  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous() && dst.numel() * dst.element_size() >= nb && nb >= 16384,
+              "cs336: occupy_bytes needs contiguous src/dst of >= 16 KiB, dst at least src's size");
+  TORCH_CHECK(n_workgroups > 0 && n_workgroups <= 4096 && lds_bytes >= 4 && lds_bytes <= 65536 && ms > 0 && ms < 10000 &&
+                  total_bytes >= 0,
+              "cs336: occupy_bytes arguments out of range");
+  c10::DeviceGuard g(src.device());
+  cs336::occupy_bytes((int)n_workgroups, (int)lds_bytes, ms, src.data_ptr(), dst.data_ptr(), nb & ~(int64_t)16383,
+                      total_bytes, counter.data_ptr<int>(), stream());
+}
+
 // co-residency probe (csrc/ops/occupy.hip), on the current stream; state: int32[3]
 void cohort(int64_t n_workgroups, int64_t lds_bytes, double deadline_ms, at::Tensor& state) {
   check_cuda(state, "state");
@@ -1351,6 +1367,7 @@ TORCH_LIBRARY(cs336, m) {
       "Tensor(d!)[] shadows, Tensor(e!)[] wts, float lr, float beta1, float beta2, float eps, float weight_decay, "
       "int step, Tensor? alpha_dev=None) -> ()");
   m.def("occupy(int n_workgroups, int lds_bytes, float ms, Tensor(a!) counter) -> ()");
+  m.def("occupy_bytes(int n_workgroups, int lds_bytes, float ms, Tensor src, Tensor(a!) dst, int total_bytes, Tensor(b!) counter) -> ()");
   m.def("cohort(int n_workgroups, int lds_bytes, float deadline_ms, Tensor(a!) state) -> ()");
   m.def("gemm8(Tensor a, Tensor b, Tensor(a!) c, int epi, int fn, Tensor(b!)? h, Tensor? y, int half) -> ()");
   m.def("gemm8_ok(int M, int N, int K, int epi, int half) -> bool", &gemm8_ok);
@@ -1393,6 +1410,7 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("embedding_bwd_into", &embedding_bwd_into);
   m.impl("multi_tensor_l2norm", &multi_tensor_l2norm);
   m.impl("occupy", &occupy);
+  m.impl("occupy_bytes", &occupy_bytes);
   m.impl("cohort", &cohort);
   m.impl("gemm8", &gemm8);
   m.impl("gemm8_rope", &gemm8_rope);

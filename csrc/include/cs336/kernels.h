@@ -37,6 +37,10 @@ void transpose16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int R
 // ---- diagnostics (csrc/ops/occupy.hip): n_workgroups x 256 threads, each holding lds_bytes of LDS,
 // spin for `ms` of wall-clock time, then atomically increment *done
 void occupy(int n_workgroups, int lds_bytes, double ms, int* done, hipStream_t s);
+// the same, moving `total_bytes` (half read from src, half written to dst, both nbytes long, cycled)
+// paced over `ms` -- the per-rank HBM traffic of a ring all-reduce (scripts/comm_emulation.py)
+void occupy_bytes(int n_workgroups, int lds_bytes, double ms, const void* src, void* dst, int64_t nbytes,
+                  int64_t total_bytes, int* done, hipStream_t s);
 // co-residency probe: n_workgroups that each wait (up to deadline_ms) until all of them have arrived;
 // state[0] arrivals (reset per launch), state[1] += workgroups that timed out, state[2] = max wait
 // in 100 MHz ticks

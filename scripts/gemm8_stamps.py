@@ -24,15 +24,25 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-# name, N, K, epi (M = tokens)
-PROBLEMS = [
-    ("o fwd", 1600, 1600, 0),
-    ("qkv fwd (plain)", 4800, 1600, 0),
-    ("w13 fwd+swiglu", 12800, 1600, 1),
-    ("w2 dX+swiglu_bwd", 6400, 1600, 2),
-    ("w2 fwd", 1600, 6400, 0),
-    ("w13 dX", 1600, 12800, 0),
-]
+# name, N, K, epi (M = tokens), per model
+PROBLEMS = {
+    "xl": [
+        ("o fwd", 1600, 1600, 0),
+        ("qkv fwd (plain)", 4800, 1600, 0),
+        ("w13 fwd+swiglu", 12800, 1600, 1),
+        ("w2 dX+swiglu_bwd", 6400, 1600, 2),
+        ("w2 fwd", 1600, 6400, 0),
+        ("w13 dX", 1600, 12800, 0),
+    ],
+    "2p7b": [
+        ("o fwd", 2560, 2560, 0),
+        ("qkv fwd (plain)", 7680, 2560, 0),
+        ("w13 fwd+swiglu", 20480, 2560, 1),
+        ("w2 dX+swiglu_bwd", 10240, 2560, 2),
+        ("w2 fwd", 2560, 10240, 0),
+        ("qkv dX", 2560, 7680, 0),
+    ],
+}
 
 
 def analyse(st: torch.Tensor) -> dict:
@@ -67,6 +77,7 @@ def analyse(st: torch.Tensor) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=52224)
+    ap.add_argument("--model", choices=sorted(PROBLEMS), default="xl")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
     from cs336_systems import ops
@@ -75,7 +86,7 @@ def main():
     cs = torch.ops.cs336
     M = args.tokens
     rows = []
-    for name, N, K, epi in PROBLEMS:
+    for name, N, K, epi in PROBLEMS[args.model]:
         g = torch.Generator(device="cuda").manual_seed(N + K)
         a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).bfloat16()
         half = N // 2 if epi == 1 else N
@@ -96,7 +107,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         cs.gemm8_stamps(None)
-        row = {"problem": name, "M": M, "N": N, "K": K, "epi": epi, "ms": round(e0.elapsed_time(e1), 4), **analyse(st)}
+        row = {"model": args.model, "problem": name, "M": M, "N": N, "K": K, "epi": epi, "ms": round(e0.elapsed_time(e1), 4), **analyse(st)}
         rows.append(row)
         print(json.dumps(row), flush=True)
         del a, b, c, h, y, st

@@ -40,7 +40,7 @@ for r in json.load(open('gpurun_out/flash4096.json')):
       timeout -k 10 600 python -u -m pytest ${QUICK_TESTS:-tests/test_train_graph_gpu.py} -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_quick.log 2>&1 || { tail -60 gpurun_out/gpu_quick.log; exit 1; }
       tail -3 gpurun_out/gpu_quick.log ;;
     stamps)  # in-kernel gemm8 phase stamps (CS336_G8_STAMP variant build)
-      CS336_LIB=cs336_systems/_native/variants/stamp/libcs336_hip.so timeout -k 10 300 python -u scripts/gemm8_stamps.py --json gpurun_out/gemm8_stamps.json > gpurun_out/gemm8_stamps.log 2>&1 || { tail -30 gpurun_out/gemm8_stamps.log; exit 1; }
+      CS336_LIB=cs336_systems/_native/variants/stamp/libcs336_hip.so timeout -k 10 300 python -u scripts/gemm8_stamps.py ${STAMP_ARGS:-} --json gpurun_out/gemm8_stamps.json > gpurun_out/gemm8_stamps.log 2>&1 || { tail -30 gpurun_out/gemm8_stamps.log; exit 1; }
       cat gpurun_out/gemm8_stamps.log ;;
     graphab)  # eager step vs the whole step captured in one HIP graph, same box
       timeout -k 10 900 python scripts/ab.py bench "eager:" "graphs:PYTHONFAULTHANDLER=1:--graphs on" --rounds ${AB_ROUNDS:-2} --steps 10 --timeout 300 > gpurun_out/graphab.log 2>&1 || { tail -30 gpurun_out/graphab.log; exit 1; }
@@ -53,6 +53,15 @@ for r in json.load(open('gpurun_out/flash4096.json')):
         done
       done
       grep '^{' gpurun_out/dwab.log ;;
+    ddpw1)  # DDP's own cost at world 1 (no collectives since round 6): plain step vs the bucketed wrapper
+      timeout -k 10 1200 python scripts/ab.py bench "plain::--overlap-opt off" "ddpw1::--ddp-world1" "ddpw1ov::--ddp-world1 --overlap-opt on" --rounds ${AB_ROUNDS:-2} --steps 10 --timeout 300 > gpurun_out/ddpw1.log 2>&1 || { tail -30 gpurun_out/ddpw1.log; exit 1; }
+      cat gpurun_out/ddpw1.log ;;
+    emul)  # emulated W = 8 communication beside the real XL backward (byte-moving occupants)
+      timeout -k 10 900 python -u scripts/comm_emulation.py ${EMUL_ARGS:-} > gpurun_out/comm_emulation.jsonl 2> gpurun_out/comm_emulation.err || { tail -30 gpurun_out/comm_emulation.err; exit 1; }
+      cat gpurun_out/comm_emulation.jsonl ;;
+    numa)  # 1-GPU bench with / without the host pinned to the GPU's NUMA-local CPUs
+      timeout -k 10 1200 python scripts/ab.py bench "pin:" "nopin:CS336_NUMA_PIN=0" "pin_ovoff::--overlap-opt off" --rounds ${AB_ROUNDS:-2} --steps 10 --timeout 300 > gpurun_out/numa.log 2>&1 || { tail -30 gpurun_out/numa.log; exit 1; }
+      cat gpurun_out/numa.log ;;
     *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done

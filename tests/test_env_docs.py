@@ -62,6 +62,7 @@ RETIRED_KNOBS = [
     r"G8_PERSIST",                # persistent gemm8 (profiles/r3_gemm8_persistent_ab.md, r5_step_clocks.md)
     r"G8_NO_EPI",
     r"G8_ABL_",                   # epilogue ablation builds (profiles/r5_gemm8_epilogue.md)
+    r"PersistentGrads|grad[-_]buffers",  # 1-GPU persistent gradient views (profiles/r6_ddp_world1.md)
 ]
 
 
