@@ -129,8 +129,11 @@ class Embedding(nn.Module):
         self.weight = nn.Parameter(_trunc_normal((vocab_size, d_model), 1.0, device, dtype), requires_grad=True)
 
     def forward(self, token_ids: torch.Tensor) -> torch.Tensor:
-        if token_ids.is_cuda and not torch.compiler.is_compiling() and (
-                ops.get_backend() != "torch" or torch.cuda.is_current_stream_capturing()):
+        if torch.compiler.is_compiling():
+            if token_ids.is_cuda and ops.get_backend() != "torch":
+                return compiled.embedding(token_ids, self.weight)  # the same HIP backward, traceable
+            return F.embedding(token_ids, self.weight)
+        if token_ids.is_cuda and (ops.get_backend() != "torch" or torch.cuda.is_current_stream_capturing()):
             return _GraphSafeEmbedding.apply(token_ids, self.weight)
         return F.embedding(token_ids, self.weight)
 

@@ -60,6 +60,11 @@ def _emb_bwd(g, sorted_ids, perm, vocab):
     return g.new_empty((vocab, g.shape[1]), dtype=torch.float32)
 
 
+@register_fake("cs336::cast_transpose_bf16")
+def _cast_t(x):
+    return x.new_empty(x.shape, dtype=torch.bfloat16), x.new_empty((x.shape[1], x.shape[0]), dtype=torch.bfloat16)
+
+
 @register_fake("cs336::transpose2d")
 def _transpose2d(x):
     return x.new_empty((x.shape[1], x.shape[0]))

@@ -542,6 +542,24 @@ at::Tensor transpose2d(const at::Tensor& x) {
 }
 
 // out = x.T into an existing (possibly column-block) view: out (C, R) with unit column stride
+// (bf16 w, bf16 wᵀ) of an fp32 2-D weight in one pass (csrc/ops/transpose.hip cast_t_kernel)
+std::tuple<at::Tensor, at::Tensor> cast_transpose_bf16(const at::Tensor& x) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.scalar_type() == at::kFloat,
+              "cs336: cast_transpose_bf16 needs a 2-D fp32 row-major tensor");
+  const int64_t R = x.size(0), C = x.size(1);
+  TORCH_CHECK(R % 8 == 0 && C % 8 == 0 && x.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                  R < INT32_MAX && C < INT32_MAX,
+              "cs336: cast_transpose_bf16 needs dims multiples of 8 and 16-B aligned rows");
+  c10::DeviceGuard g(x.device());
+  at::Tensor w = at::empty({R, C}, x.options().dtype(at::kBFloat16));
+  at::Tensor wt = at::empty({C, R}, x.options().dtype(at::kBFloat16));
+  if (R > 0 && C > 0)
+    cs336::cast_transpose_bf16(x.data_ptr<float>(), x.stride(0), w.data_ptr(), C, wt.data_ptr(), R, (int)R, (int)C,
+                               stream());
+  return {w, wt};
+}
+
 void transpose2d_into(const at::Tensor& x, at::Tensor& out) {
   check_cuda(x, "x");
   check_cuda(out, "out");
@@ -1358,6 +1376,7 @@ TORCH_LIBRARY(cs336, m) {
       "Tensor? alpha_dev=None) -> ()");
   m.def("adamw_device_step(Tensor(a!) t, Tensor(b!) alpha, float lr, float beta1, float beta2) -> ()");
   m.def("embedding_bwd(Tensor g, Tensor sorted_ids, Tensor perm, int vocab) -> Tensor");
+  m.def("cast_transpose_bf16(Tensor x) -> (Tensor, Tensor)");
   m.def("gemm8_stamps(Tensor? buf) -> bool", &gemm8_stamps);
   m.def("embedding_bwd_into(Tensor g, Tensor sorted_ids, Tensor perm, Tensor(a!) out) -> ()");
   m.def("multi_tensor_l2norm(Tensor[] tensors) -> Tensor");
@@ -1407,6 +1426,7 @@ TORCH_LIBRARY_IMPL(cs336, CUDA, m) {
   m.impl("adamw_step_t", &adamw_step_t);
   m.impl("adamw_device_step", &adamw_device_step);
   m.impl("embedding_bwd", &embedding_bwd);
+  m.impl("cast_transpose_bf16", &cast_transpose_bf16);
   m.impl("embedding_bwd_into", &embedding_bwd_into);
   m.impl("multi_tensor_l2norm", &multi_tensor_l2norm);
   m.impl("occupy", &occupy);

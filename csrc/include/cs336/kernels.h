@@ -33,6 +33,9 @@ void rmsnorm_bwd_add(const void* dy, DType dyt, const void* x, DType xt, const f
 // ---- 2-byte transpose (csrc/ops/transpose.hip): out[c][r] = in[r][c]; R, C multiples of 8,
 // 16-B aligned rows
 void transpose16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int R, int C, hipStream_t s);
+// fp32 [R][C] -> bf16 w [R][C] and its transpose wt [C][R] in one pass (R, C multiples of 8, 16-B rows)
+void cast_transpose_bf16(const float* in, int64_t ld_in, void* w, int64_t ld_w, void* wt, int64_t ld_t, int R, int C,
+                         hipStream_t s);
 
 // ---- diagnostics (csrc/ops/occupy.hip): n_workgroups x 256 threads, each holding lds_bytes of LDS,
 // spin for `ms` of wall-clock time, then atomically increment *done

@@ -47,7 +47,47 @@ __global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* __rest
   }
 }
 
+// fp32 -> bf16 cast that also writes the transpose: w[r][c] = bf16(in[r][c]), wt[c][r] = the same.
+// Same 8x8-per-thread register transpose as above; 4 B read + 4 B written per element (a cast and a
+// separate 16-bit transpose move 10). The compiled model's projections use it for their bf16
+// compute weight and the K-major Wᵀ their input gradient reads when no bf16 shadows are attached
+// (models/compiled.py).
+__global__ __launch_bounds__(256) void cast_t_kernel(const float* __restrict__ in, int64_t ld_in,
+                                                     uint16_t* __restrict__ w, int64_t ld_w,
+                                                     uint16_t* __restrict__ wt, int64_t ld_t, int R, int C) {
+  const int tid = threadIdx.x, ch = tid & 7, rr = tid >> 3;
+  const int r = blockIdx.y * kRows + 8 * rr;
+  const int c = blockIdx.x * kCols + 8 * ch;
+  if (r >= R || c >= C) return;  // R, C multiples of 8 (host check)
+  uint32_t v[8][4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float4 a = *reinterpret_cast<const float4*>(in + (int64_t)(r + j) * ld_in + c);
+    const float4 b = *reinterpret_cast<const float4*>(in + (int64_t)(r + j) * ld_in + c + 4);
+    v[j][0] = (uint32_t)f32_to_bf16(a.x) | ((uint32_t)f32_to_bf16(a.y) << 16);
+    v[j][1] = (uint32_t)f32_to_bf16(a.z) | ((uint32_t)f32_to_bf16(a.w) << 16);
+    v[j][2] = (uint32_t)f32_to_bf16(b.x) | ((uint32_t)f32_to_bf16(b.y) << 16);
+    v[j][3] = (uint32_t)f32_to_bf16(b.z) | ((uint32_t)f32_to_bf16(b.w) << 16);
+    *reinterpret_cast<uint4*>(w + (int64_t)(r + j) * ld_w + c) = make_uint4(v[j][0], v[j][1], v[j][2], v[j][3]);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int d = k >> 1;
+    uint32_t o[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      o[p] = (k & 1) ? hi_pair(v[2 * p][d], v[2 * p + 1][d]) : lo_pair(v[2 * p][d], v[2 * p + 1][d]);
+    *reinterpret_cast<uint4*>(wt + (int64_t)(c + k) * ld_t + r) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 }  // namespace
+
+void cast_transpose_bf16(const float* in, int64_t ld_in, void* w, int64_t ld_w, void* wt, int64_t ld_t, int R, int C,
+                         hipStream_t s) {
+  const dim3 grid((unsigned)((C + kCols - 1) / kCols), (unsigned)((R + kRows - 1) / kRows)), block(256);
+  hipLaunchKernelGGL(cast_t_kernel, grid, block, 0, s, in, ld_in, (uint16_t*)w, ld_w, (uint16_t*)wt, ld_t, R, C);
+}
 
 // (the round-1 64x64 LDS-tile version, CS336_TRANSPOSE=lds, was retired in round 5:
 // profiles/r1_transpose_reg_vs_lds.md)

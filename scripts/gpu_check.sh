@@ -62,6 +62,14 @@ for r in json.load(open('gpurun_out/flash4096.json')):
     numa)  # 1-GPU bench with / without the host pinned to the GPU's NUMA-local CPUs
       timeout -k 10 1200 python scripts/ab.py bench "pin:" "nopin:CS336_NUMA_PIN=0" "pin_ovoff::--overlap-opt off" --rounds ${AB_ROUNDS:-2} --steps 10 --timeout 300 > gpurun_out/numa.log 2>&1 || { tail -30 gpurun_out/numa.log; exit 1; }
       cat gpurun_out/numa.log ;;
+    cveprof)  # kernel traces of the eager and the compiled e2e step (CVE_SIZE, batch 4, ctx 512)
+      cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+      for m in eager compile; do
+        flag=""; [ $m = compile ] && flag="--compile"
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/cve_$m -o run -- python -u -m cs336_systems.bench.e2e --sizes ${CVE_SIZE:-2.7b} --ctx 512 --mixed $flag --json gpurun_out/cve_$m.json > gpurun_out/cve_$m.log 2>&1 || { tail -20 gpurun_out/cve_$m.log; exit 1; }
+        cp $(find gpurun_out/cve_$m -name '*kernel_stats.csv' | head -n1) gpurun_out/cve_${m}_kernel_stats.csv
+        cat gpurun_out/cve_$m.json
+      done ;;
     *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done
