@@ -6,6 +6,8 @@ that are not multiples of the 256 x 64 workgroup tile."""
 import pytest
 import torch
 
+from cs336_systems.ops._ext import ops as _hip
+
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
@@ -14,7 +16,7 @@ DEV = "cuda"
 def test_cast_transpose_matches_torch(R, C):
     torch.manual_seed(R + C)
     x = torch.randn(R, C, device=DEV) * 3
-    w, wt = torch.ops.cs336.cast_transpose_bf16(x)
+    w, wt = _hip().cast_transpose_bf16(x)
     ref = x.to(torch.bfloat16)
     assert torch.equal(w, ref)
     assert torch.equal(wt, ref.t().contiguous())
@@ -23,5 +25,5 @@ def test_cast_transpose_matches_torch(R, C):
 def test_cast_transpose_of_row_block_view():
     big = torch.randn(3 * 640, 1600, device=DEV)
     v = big[640:1920]  # row-adjacent block (a grouped weight view)
-    w, wt = torch.ops.cs336.cast_transpose_bf16(v)
+    w, wt = _hip().cast_transpose_bf16(v)
     assert torch.equal(w, v.to(torch.bfloat16)) and torch.equal(wt, v.to(torch.bfloat16).t().contiguous())
