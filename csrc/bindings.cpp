@@ -255,7 +255,7 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
   //          (B·H >= 512): fa_bwd_hs.hip (d 64, N <= 1024, N % 128 == 0), else fa_bwd_fused.hip
   //          (d 64, N <= 1024: the N % 128 == 64 shapes, 1.37x the two-kernel form,
   //          profiles/r5_fa_bwd_forms.md); else at d 80 the key-block-parallel fused
-  //          kernel (fa_bwd_kp.hip, dQ by fp32 atomics), else the two-kernel form (split over keys /
+  //          kernel (fa_bwd_kp.hip, dQ by slabs / fp32 atomics), else the two-kernel form (split over keys /
   //          queries at low parallelism);
   //   1: head-sequential wherever it applies (then as unset); 2: key-block parallel wherever it
   //   applies; 0: the two-kernel form (dQ kernel + dK/dV kernel: deterministic, any shape);
@@ -324,9 +324,9 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
     }
     bp.dq_acc = nullptr;
   }
-  // key-block parallel: forced by mode 2; by default only at d 80 (the 2.7b model), where it beats the
-  // two-kernel form (N 4096 causal 466 vs 446 TF, 2.7b step 269 vs 272 ms). At d 64 its dQ atomics
-  // bound it below the two-kernel form (513 vs 625 TF at N 4096 causal): profiles/r4_fa_kp.md
+  // key-block parallel: forced by mode 2; by default only at d 80 (the 2.7b model), where its 8-wave
+  // causal form beats the two-kernel form (B 32 H 32 N 1024 1.11 vs 1.35 ms, N 4096 617 vs 445 TF;
+  // profiles/r6_fa_kp_waves.md). At d 64 the two-kernel form stays ahead at N 4096 (r4_fa_kp.md, ibid.)
   if ((mode == 2 || (mode < 0 && q.size(3) == 80)) && cs336::flash_attn_bwd_kp_ok(bp, to_dtype(q))) {
     at::Tensor ws = at::empty({(int64_t)cs336::flash_attn_bwd_kp_workspace(bp)}, q.options().dtype(at::kFloat));
     cs336::flash_attn_bwd_kp(bp, to_dtype(q), ws.data_ptr<float>(), stream());

@@ -9,29 +9,32 @@
 // full N x N matrices; handout Algorithm 2). fa_bwd.hip's two-kernel form computes S and dP in both
 // kernels (7 GEMM-equivalents per tile pair); this one computes them once.
 //
-// Why atomics here (cdna_hip_programming.md "Attention backward"): with a 256-key block per
-// workgroup the dQ sum costs one byte of f32 adds per 640 FLOPs, i.e. a floor of ~830 TFLOP/s at
-// the chip-wide atomic rate (MI355X_MICROARCH.md "Global float atomics", 1.3 TB/s), above what the
-// MFMA work of this structure reaches. Each dQ tile leaves as 16 no-return global_atomic_add_f32
-// per wave, one accumulator register each = two 128-B row segments (the full-rate shape).
-// The sums are not bitwise reproducible run to run (fp32 add order); CS336_FA_BWD=0 selects the
-// deterministic two-kernel form.
+// The dQ sum across key blocks: up to 4 key blocks (N <= 1024, the 2.7b step) each block writes its
+// dQ contribution with plain stores into its own fp32 slab (slab kb holds rows kbase.. under the
+// causal mask, every row otherwise) and the convert launch sums the slabs in key-block order --
+// deterministic, and 4.5 % faster than atomics there. Longer sequences use no-return
+// global_atomic_add_f32 into one zeroed accumulator (16 per tile and wave, one accumulator register
+// each = two 128-B row segments, the full-rate shape; not bitwise reproducible): the convert would
+// read nkb / 2 slabs per row.
 //
 // Launches: (1) prep: per query row -lse·log2(e) and -delta (delta = rowsum(dO·O)) in the row order
-// the accumulators want (row_perm), and the fp32 dQ accumulator zeroed; (2) the main kernel;
-// (3) dQ = scale · acc cast to the output dtype (inverse RoPE folded in when q was rotated).
+// the accumulators want (row_perm) (+ the atomic accumulator zeroed); (2) the main kernel;
+// (3) dQ = scale · (sum of the slabs | acc) cast to the output dtype (inverse RoPE folded in when q
+// was rotated).
 //
-// Main kernel structure: 4 waves (one per SIMD, up to 512 registers each), wave w owns keys
-// 64w .. 64w+63 of the block as two 32-key groups (key on the MFMA lane), keeping dKᵀ / dVᵀ of its
-// 64 keys and V (B operand of dP) in registers; K lives in one LDS image read by rows (S) and by
+// Main kernel structure: WV = 8 waves (two per SIMD, <= 256 registers each; the causal default) or 4
+// (one per SIMD, up to 512 registers), wave w owns 32 keys (8 waves) or 64 keys as two 32-key groups
+// (4 waves) of the block (key on the MFMA lane), keeping dKᵀ / dVᵀ of its keys and V (B operand of
+// dP) in registers; K lives in one LDS image read by rows (S) and by
 // columns (dQ). The workgroup sweeps 64-row query slices (Q, dO and the slice's row constants staged
 // by LDS-DMA in a 3-slot ring, two slices ahead); per 32-query tile and group:
 //   S = Q Kᵀ, dP = dO Vᵀ - delta (row constant as the accumulator's start), P = exp2(S c - L),
 //   dS = P dP, dVᵀ += dOᵀ P, dKᵀ += Qᵀ dS (accumulators as B operands, dOᵀ / Qᵀ by transposed LDS
 //   reads of the same slot images), dSᵀ -> LDS;
 // barrier; each wave forms its dQ tile(s) (32 q x 32 d) = dS K over the active keys (both operands
-// transposed reads) and issues their atomics at the start of the next slice, so a slice's DMA wait
-// stays a compile-time count (atomics and DMA share vmcnt, which retires in issue order).
+// transposed reads) and issues their stores / atomics at the start of the next slice, so a slice's DMA
+// wait stays a compile-time count (stores and DMA share vmcnt, which retires in issue order). Waves 0-3
+// stage the slices (TileDma's 4 x 64-lane rounds); with 8 waves, waves 4-7 issue no DMA.
 // Causal: key block 0 (the heaviest) of every head is dispatched first; the slices start at the
 // block's diagonal and only diagonal tiles are masked.
 #include "fa_common.h"
@@ -42,9 +45,30 @@ namespace fa {
 namespace {
 constexpr int KP_KB = 256;  // keys per workgroup
 constexpr int KP_BQ = 64;   // query slice
+constexpr int64_t KP_SLAB_LIMIT = (int64_t)4 << 30;  // bytes of dQ slabs before the atomic fallback
 
-template <int D>
+// waves per workgroup: 4 (one per SIMD, 64 keys = two 32-key groups each) or 8 (two per SIMD, one group
+// each: a second wave on every SIMD covers the first one's LDS and barrier latencies). 8 under the
+// causal mask, 4 without it (there the d 80 8-wave build spills); CS336_FA_KP_WAVES=4|8 forces one.
+inline int kp_waves(const AttnBwdParams& bp) {
+  const char* e = getenv("CS336_FA_KP_WAVES");
+  if (e && *e) return atoi(e) == 8 ? 8 : 4;
+  return bp.f.causal ? 8 : 4;
+}
+
+inline int kp_nkb(const AttnBwdParams& bp) { return (bp.f.Nq + KP_KB - 1) / KP_KB; }
+// slabs up to 4 key blocks (N <= 1024): B 32 H 32 N 1024 d 80 causal 1.11 vs 1.16 ms with atomics;
+// at N 4096 (16 blocks; the convert then reads 8.5 slabs per row) atomics win, 0.70 vs 0.80 ms
+// (profiles/r6_fa_kp_waves.md). CS336_FA_KP_SLAB=0|1 forces one (slabs only within KP_SLAB_LIMIT).
+inline bool kp_slabs(const AttnBwdParams& bp) {
+  const char* e = getenv("CS336_FA_KP_SLAB");
+  const bool want = (e && *e) ? atoi(e) != 0 : kp_nkb(bp) <= 4;
+  return want && (int64_t)kp_nkb(bp) * bp.f.B * bp.f.H * bp.f.Nq * bp.f.D * 4 <= KP_SLAB_LIMIT;
+}
+
+template <int D, int WV>
 struct KpGeo {
+  static constexpr int GPW = 8 / WV;            // 32-key groups per wave
   static constexpr int DP = PadD<D>::value;     // compute width (80 -> 96: d >= D zero in the images)
   static constexpr int RB = DP * 2;             // Q / dO / K image row bytes
   static constexpr int CPR = RB / 16;
@@ -59,9 +83,10 @@ struct KpGeo {
   static constexpr int NQT = 2 * NDT;                // dQ tiles (32 q x 32 d) per slice
   static constexpr int SLICE_DMA = 2 * (KP_BQ * CPR / 256);  // Q + dO wave-instructions per wave
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  // dQ tiles of wave w (w, w + 4 < NQT) and the vmcnt a slice's wait may leave in flight: this wave's
-  // atomics of the previous slice (issued after that slice's DMA) + the next slice's DMA
-  static constexpr int tiles(int w) { return (w < NQT ? 1 : 0) + (w + 4 < NQT ? 1 : 0); }
+  // dQ tiles of wave w (w, w + WV, ... < NQT) and the vmcnt a slice's wait may leave in flight: this
+  // wave's dQ stores of the previous slice (issued after that slice's DMA) + the next slice's DMA
+  // (waves 0-3 stage the slices: TileDma's 4 x 64-lane rounds)
+  static constexpr int tiles(int w) { return (w < NQT ? 1 : 0) + (w + WV < NQT ? 1 : 0) + (w + 2 * WV < NQT ? 1 : 0); }
   static constexpr int inflight(int w) { return 16 * tiles(w) + SLICE_DMA + (w == 0 ? 1 : 0); }
   static_assert(inflight(0) <= 63, "vmcnt range");
 };
@@ -80,7 +105,7 @@ __device__ __forceinline__ void tr_offsets(int lane, int c, uint32_t& oa, uint32
 
 // ---- (1) row constants + zeroed dQ accumulator ------------------------------------------------
 // block = (head, 64-row slice); 4 threads per row, each over 16-B chunks c, c+4, ... of d
-template <typename T, int D>
+template <typename T, int D, bool SLAB>
 __global__ __launch_bounds__(256) void fa_bwd_kp_prep(const AttnBwdParams bp, float* __restrict__ rowc,
                                                       float* __restrict__ acc) {
   typedef typename Elem<T>::storage S;
@@ -109,15 +134,18 @@ __global__ __launch_bounds__(256) void fa_bwd_kp_prep(const AttnBwdParams bp, fl
     rc[row_perm(r)] = -bp.f.lse[(int64_t)bh * N + row] * kLog2e;
     rc[64 + row_perm(r)] = -dsum;
   }
-  float4* z = reinterpret_cast<float4*>(acc + ((int64_t)bh * N + s * KP_BQ) * D);
-  for (int i = tid; i < KP_BQ * D / 4; i += 256) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (!SLAB) {
+    float4* z = reinterpret_cast<float4*>(acc + ((int64_t)bh * N + s * KP_BQ) * D);
+    for (int i = tid; i < KP_BQ * D / 4; i += 256) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
 }
 
 // ---- (2) main kernel ---------------------------------------------------------------------------
-template <typename T, int D, bool CAUSAL, bool ROPE>
-__global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams bp, const float* __restrict__ rowc,
-                                                           float* __restrict__ acc) {
-  using G = KpGeo<D>;
+template <typename T, int D, bool CAUSAL, bool ROPE, bool SLAB, int WV>
+__global__ __launch_bounds__(64 * WV, 1) void fa_bwd_kp_kernel(const AttnBwdParams bp, const float* __restrict__ rowc,
+                                                               float* __restrict__ acc) {
+  using G = KpGeo<D, WV>;
+  constexpr int GPW = G::GPW;
   typedef typename Elem<T>::storage S;
   typedef typename Mma16<T>::frag F;
   constexpr int DP = G::DP, RB = G::RB, NDT = G::NDT, NKS = G::NKS, CREAL = G::CREAL;
@@ -140,7 +168,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
   if constexpr (DP != D) {
     // d 80 runs as 96: the pad columns of every image must read as zeros (the DMA never writes them);
     // all of LDS is zeroed before any wave issues a DMA into it
-    for (int o = tid * 16; o < G::LDS; o += 256 * 16) *reinterpret_cast<uint4*>(smem + o) = make_uint4(0, 0, 0, 0);
+    for (int o = tid * 16; o < G::LDS; o += 64 * WV * 16) *reinterpret_cast<uint4*>(smem + o) = make_uint4(0, 0, 0, 0);
     __syncthreads();
   }
 
@@ -166,14 +194,16 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
   };
 
   // ---- LDS-DMA staging --------------------------------------------------------------------------
-  TileDma<KP_BQ, RB, CREAL, 2> dq_, dd_;  // Q / dO slices
-  dq_.init(wave, lane, bp.f.q_sn);
-  dd_.init(wave, lane, bp.do_sn);
+  TileDma<KP_BQ, RB, CREAL, 2> dq_, dd_;  // Q / dO slices (waves 0-3)
+  const bool stager = WV == 4 || wave < 4;
+  dq_.init(wave & 3, lane, bp.f.q_sn);
+  dd_.init(wave & 3, lane, bp.do_sn);
   const int64_t nrc = (int64_t)nqs * 512;  // this head's row constants: 512 B per slice
   const __amdgpu_buffer_rsrc_t rrc = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(rowc + (int64_t)bh * nqs * 128), (short)0, (int)nrc, 0x00020000);
   const uint32_t vrc = lane < 32 ? (uint32_t)(lane * 16) : 0x80000000u;  // lanes 32-63: out of range
   auto issue_slot = [&](int s, int slot) {
+    if (!stager) return;
     char* base = smem + slot * G::SLOT;
     dq_.issue(Qp + (int64_t)s * KP_BQ * bp.f.q_sn, KP_BQ, bp.f.q_sn, base, wave);
     dd_.issue(dOp + (int64_t)s * KP_BQ * bp.do_sn, KP_BQ, bp.do_sn, base + G::TILE, wave);
@@ -183,18 +213,20 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
   char* const dsimg = smem + G::OFF_DS;
   {
     TileDma<KP_KB, RB, CREAL, 2> dk_;
-    dk_.init(wave, lane, bp.f.k_sn);
-    dk_.issue(Kp + (int64_t)kbase * bp.f.k_sn, min(KP_KB, N - kbase), bp.f.k_sn, Kimg, wave);
+    if (stager) {
+      dk_.init(wave, lane, bp.f.k_sn);
+      dk_.issue(Kp + (int64_t)kbase * bp.f.k_sn, min(KP_KB, N - kbase), bp.f.k_sn, Kimg, wave);
+    }
   }
   const int s0 = CAUSAL ? kbase / KP_BQ : 0;
   if (s0 < nqs) issue_slot(s0, 0);
   if (s0 + 1 < nqs) issue_slot(s0 + 1, 1);
 
-  // ---- per-wave state: keys kw + 32g + l32, g = 0, 1 ---------------------------------------------
-  const int kw = kbase + 64 * wave;
-  uint4 vf[2][NKS];  // V as the B operand of dP (key on the lane), d = 16ks + 8hh .. +7
+  // ---- per-wave state: keys kw + 32g + l32, g < GPW ------------------------------------------------
+  const int kw = kbase + 32 * GPW * wave;
+  uint4 vf[GPW][NKS];  // V as the B operand of dP (key on the lane), d = 16ks + 8hh .. +7
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < GPW; ++g) {
     const int key = min(kw + 32 * g + l32, N - 1);  // keys >= N: whole skipped groups (N % 64 == 0)
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
@@ -203,9 +235,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
                                      : make_uint4(0, 0, 0, 0);
     }
   }
-  f32x16 dk[2][NDT], dv[2][NDT];
+  f32x16 dk[GPW][NDT], dv[GPW][NDT];
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+  for (int g = 0; g < GPW; ++g)
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
       dk[g][dt] = zero16();
@@ -215,18 +247,22 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
   constexpr int MT = G::tiles(0);
   f32x16 dqp[MT];
   int dq_row0 = -1;  // first query row of the pending slice (-1: none)
-  float* const accb = acc + (int64_t)bh * N * D;
+  float* const accb = acc + ((SLAB ? (int64_t)kb * BH : 0) + bh) * N * D;  // this block's slab | the accumulator
   auto flush_dq = [&]() {
     if (dq_row0 < 0) return;
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      const int tq = wave + 4 * i;
+      const int tq = wave + WV * i;
       if (tq >= G::NQT) break;
       const int qq = tq / NDT, dt = tq % NDT, d = 32 * dt + l32;
       float* p = accb + (int64_t)(dq_row0 + 32 * qq + 4 * hh) * D + d;
       if (DP == D || d < D) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) unsafeAtomicAdd(p + (int64_t)((r & 3) + 8 * (r >> 2)) * D, dqp[i][r]);
+        for (int r = 0; r < 16; ++r) {
+          float* pr = p + (int64_t)((r & 3) + 8 * (r >> 2)) * D;
+          if constexpr (SLAB) *pr = dqp[i][r];
+          else unsafeAtomicAdd(pr, dqp[i][r]);
+        }
       }
     }
   };
@@ -246,7 +282,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
     if (wave == 0) wait_vmcnt<G::inflight(0)>();
     else if (wave == 1) wait_vmcnt<G::inflight(1)>();
     else if (wave == 2) wait_vmcnt<G::inflight(2)>();
-    else wait_vmcnt<G::inflight(3)>();
+    else if (wave == 3) wait_vmcnt<G::inflight(3)>();  // (waves 4-7 stage nothing)
     dma_barrier();
     // B: the previous slice's dQ atomics, then the slice two ahead (ring slot of the previous slice)
     flush_dq();
@@ -256,16 +292,17 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int qt0 = q0 + 32 * t;
-      bool act[2];
+      bool act[GPW], any = false;
 #pragma unroll
-      for (int g = 0; g < 2; ++g) {
+      for (int g = 0; g < GPW; ++g) {
         const int key0 = kw + 32 * g;
         act[g] = key0 < N && (!CAUSAL || key0 <= qt0 + 31);
+        any = any || act[g];
       }
-      if (!act[0] && !act[1]) continue;
+      if (!any) continue;
       const char* Qt = Qs + 32 * t * RB;
       const char* dOt = dOs + 32 * t * RB;
-      f32x16 sa[2], dp[2];
+      f32x16 sa[GPW], dp[GPW];
       {
         F qa[NKS], oa[NKS];
 #pragma unroll
@@ -274,9 +311,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
           oa[ks] = rowf(dOt, ks);
         }
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < GPW; ++g) {
           if (!act[g]) continue;
-          const char* Kg = Kimg + (64 * wave + 32 * g) * RB;
+          const char* Kg = Kimg + (32 * (GPW * wave + g)) * RB;
           dp[g] = *reinterpret_cast<const f32x16*>(Ds + 32 * t + 16 * hh);
           sa[g] = zero16();
 #pragma unroll
@@ -286,9 +323,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
           }
         }
       }
-      F pf[2][2], sf[2][2];
+      F pf[GPW][2], sf[GPW][2];
 #pragma unroll
-      for (int g = 0; g < 2; ++g) {
+      for (int g = 0; g < GPW; ++g) {
         if (!act[g]) continue;
         const int key0 = kw + 32 * g;
         const bool diag = CAUSAL && key0 + 31 > qt0;
@@ -310,8 +347,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
         pf[g][1] = pack_acc<T>(sa[g], 1);
         sf[g][0] = pack_acc<T>(dp[g], 0);
         sf[g][1] = pack_acc<T>(dp[g], 1);
-        // dSᵀ rows (block-local key 64w + 32g + l32): query halves 16s2 + 4hh + 0..3 and + 8
-        char* drow = dsimg + (64 * wave + 32 * g + l32) * 128 + 8 * hh;
+        // dSᵀ rows (block-local key 32 (GPW w + g) + l32): query halves 16s2 + 4hh + 0..3 and + 8
+        char* drow = dsimg + (32 * (GPW * wave + g) + l32) * 128 + 8 * hh;
         const int swl = swz<128>(l32);
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
@@ -331,7 +368,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
           qt[s2] = trf2(Qt + 16 * s2 * RB, toa[dt], tob[dt]);
         }
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < GPW; ++g) {
           if (!act[g]) continue;
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
@@ -346,7 +383,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
     // E: dQ tiles (32 q x 32 d) = dS K over the keys active for their query tile; atomics next slice
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      const int tq = wave + 4 * i;
+      const int tq = wave + WV * i;
       if (tq >= G::NQT) break;
       const int qq = tq / NDT, dt = tq % NDT;
       const int ng = CAUSAL ? min(8, (q0 + 32 * qq + 32 - kbase) / 32) : 8;
@@ -370,7 +407,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
   // ---- dK (x scale), dV of this wave's keys: lane = key, registers = d 32dt + 8g4 + 4hh + 0..3 ----
   const Rope rope{bp.f.rope_cos, bp.f.rope_sin, D / 2};
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < GPW; ++g) {
     const int key = kw + 32 * g + l32;
     if (key >= N) continue;
     S* rk = (S*)bp.dk + b * bp.dk_sb + h * bp.dk_sh + (int64_t)key * bp.dk_sn;
@@ -392,8 +429,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kp_kernel(const AttnBwdParams b
   }
 }
 
-// ---- (3) dQ = scale · acc (inverse RoPE when q was rotated), cast to the output dtype -------------
-template <typename T, int D, bool ROPE>
+// ---- (3) dQ = scale · (slabs summed in key-block order | acc) (inverse RoPE when q was rotated), cast
+// to the output dtype ---------------------------------------------------------------------------------
+template <typename T, int D, bool ROPE, bool SLAB>
 __global__ __launch_bounds__(256) void fa_bwd_kp_dq(const AttnBwdParams bp, const float* __restrict__ acc) {
   typedef typename Elem<T>::storage S;
   constexpr int Q4 = D / 4;
@@ -405,7 +443,19 @@ __global__ __launch_bounds__(256) void fa_bwd_kp_dq(const AttnBwdParams bp, cons
   const int d = 4 * (int)(gid % Q4);
   const int bh = (int)(row / N), n = (int)(row % N);
   const int b = bh / bp.f.H, h = bh % bp.f.H;
-  const float4 a = *reinterpret_cast<const float4*>(acc + row * D + d);
+  float4 a = *reinterpret_cast<const float4*>(acc + row * D + d);
+  if constexpr (SLAB) {
+    // slab kb holds this row when the row is not masked out of key block kb entirely
+    const int nkb = (N + KP_KB - 1) / KP_KB, kbn = bp.f.causal ? n / KP_KB + 1 : nkb;
+    const int64_t slab = total * 4;  // B·H·N·D floats
+    for (int kb = 1; kb < kbn; ++kb) {
+      const float4 x = *reinterpret_cast<const float4*>(acc + kb * slab + row * D + d);
+      a.x += x.x;
+      a.y += x.y;
+      a.z += x.z;
+      a.w += x.w;
+    }
+  }
   const float sc = bp.f.scale;
   float v0 = a.x * sc, v1 = a.y * sc, v2 = a.z * sc, v3 = a.w * sc;
   if constexpr (ROPE) {
@@ -416,15 +466,26 @@ __global__ __launch_bounds__(256) void fa_bwd_kp_dq(const AttnBwdParams bp, cons
   store4<T>((S*)bp.dq + b * bp.dq_sb + h * bp.dq_sh + (int64_t)n * bp.dq_sn + d, make_float4(v0, v1, v2, v3));
 }
 
-template <typename T, int D, bool ROPE>
+template <typename T, int D, bool ROPE, bool SLAB>
 void launch_kp(const AttnBwdParams& bp, float* rowc, float* acc, hipStream_t s) {
   const int BH = bp.f.B * bp.f.H, N = bp.f.Nq;
-  hipLaunchKernelGGL((fa_bwd_kp_prep<T, D>), dim3((unsigned)(BH * (N / KP_BQ))), dim3(256), 0, s, bp, rowc, acc);
-  const dim3 grid((unsigned)(BH * ((N + KP_KB - 1) / KP_KB)));
-  if (bp.f.causal) hipLaunchKernelGGL((fa_bwd_kp_kernel<T, D, true, ROPE>), grid, dim3(256), 0, s, bp, rowc, acc);
-  else hipLaunchKernelGGL((fa_bwd_kp_kernel<T, D, false, ROPE>), grid, dim3(256), 0, s, bp, rowc, acc);
+  hipLaunchKernelGGL((fa_bwd_kp_prep<T, D, SLAB>), dim3((unsigned)(BH * (N / KP_BQ))), dim3(256), 0, s, bp, rowc, acc);
+  const dim3 grid((unsigned)(BH * kp_nkb(bp)));
+  if (kp_waves(bp) == 8) {
+    if (bp.f.causal) hipLaunchKernelGGL((fa_bwd_kp_kernel<T, D, true, ROPE, SLAB, 8>), grid, dim3(512), 0, s, bp, rowc, acc);
+    else hipLaunchKernelGGL((fa_bwd_kp_kernel<T, D, false, ROPE, SLAB, 8>), grid, dim3(512), 0, s, bp, rowc, acc);
+  } else {
+    if (bp.f.causal) hipLaunchKernelGGL((fa_bwd_kp_kernel<T, D, true, ROPE, SLAB, 4>), grid, dim3(256), 0, s, bp, rowc, acc);
+    else hipLaunchKernelGGL((fa_bwd_kp_kernel<T, D, false, ROPE, SLAB, 4>), grid, dim3(256), 0, s, bp, rowc, acc);
+  }
   const int64_t quads = (int64_t)BH * N * (D / 4);
-  hipLaunchKernelGGL((fa_bwd_kp_dq<T, D, ROPE>), dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, bp, acc);
+  hipLaunchKernelGGL((fa_bwd_kp_dq<T, D, ROPE, SLAB>), dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, bp, acc);
+}
+
+template <typename T, int D, bool ROPE>
+void launch_kp(const AttnBwdParams& bp, float* rowc, float* acc, hipStream_t s) {
+  if (kp_slabs(bp)) launch_kp<T, D, ROPE, true>(bp, rowc, acc, s);
+  else launch_kp<T, D, ROPE, false>(bp, rowc, acc, s);
 }
 
 template <typename T>
@@ -456,7 +517,8 @@ bool flash_attn_bwd_kp_ok(const AttnBwdParams& bp, DType t) {
 
 size_t flash_attn_bwd_kp_workspace(const AttnBwdParams& bp) {
   const size_t rows = (size_t)bp.f.B * bp.f.H * bp.f.Nq;
-  return rows * 2 + rows * (size_t)bp.f.D;  // floats: row constants + dQ accumulator
+  const size_t nacc = fa::kp_slabs(bp) ? (size_t)fa::kp_nkb(bp) : 1;
+  return rows * 2 + nacc * rows * (size_t)bp.f.D;  // floats: row constants + dQ slabs | accumulator
 }
 
 void flash_attn_bwd_kp(const AttnBwdParams& bp, DType t, float* ws, hipStream_t s) {

@@ -70,6 +70,17 @@ for r in json.load(open('gpurun_out/flash4096.json')):
         cp $(find gpurun_out/cve_$m -name '*kernel_stats.csv' | head -n1) gpurun_out/cve_${m}_kernel_stats.csv
         cat gpurun_out/cve_$m.json
       done ;;
+    faab)  # FA2 arms (FA_ARMS: ab.py arm specs, ';'-separated) over shapes (FA_SHAPES: bench.flash arg sets, ';'-separated)
+      IFS=';' read -ra arms <<< "${FA_ARMS:-default:}"
+      IFS=';' read -ra shapes <<< "${FA_SHAPES:---seq 1024 --batch 32 --heads 32 --d 80 --causal 1}"
+      for sh in "${shapes[@]}"; do
+        timeout -k 10 900 python scripts/ab.py flash "${arms[@]}" --args "$sh" --rounds 2 --timeout 240 > gpurun_out/faab.log 2>&1 || { tail -30 gpurun_out/faab.log; exit 1; }
+        grep '^round' gpurun_out/faab.log | sed 's/hip_fa2 //' | cut -c1-150 | tee -a gpurun_out/faab_all.log
+      done ;;
+    benchab)  # bench.py arms (BENCH_ARMS, ';'-separated) with BENCH_ARGS for every arm
+      IFS=';' read -ra arms <<< "${BENCH_ARMS:-default:}"
+      timeout -k 10 1200 python scripts/ab.py bench "${arms[@]}" --args "${BENCH_ARGS:-}" --rounds ${AB_ROUNDS:-2} --steps 10 --timeout 300 > gpurun_out/benchab.log 2>&1 || { tail -30 gpurun_out/benchab.log; exit 1; }
+      grep '^round' gpurun_out/benchab.log ;;
     *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done

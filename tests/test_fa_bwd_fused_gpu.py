@@ -1,6 +1,6 @@
 """The one-kernel FlashAttention-2 backwards (csrc/flash_attn/fa_bwd_fused.hip: one 8-wave workgroup
 per (batch, head); fa_bwd_hs.hip: one 4-wave workgroup per (batch, head), two per CU; fa_bwd_kp.hip:
-one workgroup per key block, dQ by atomics) against an fp64 reference, the two-kernel backward, and
+one workgroup per key block, dQ by per-key-block slabs or atomics) against an fp64 reference, the two-kernel backward, and
 the default selection (head-sequential at B·H >= 512)."""
 
 import math
@@ -101,7 +101,8 @@ def test_fused_rope_out_only_in_step_layout(monkeypatch):
     torch.testing.assert_close(hs.float(), two.float(), rtol=2e-2, atol=2e-2)
 
 
-# ---- key-block-parallel fused backward (csrc/flash_attn/fa_bwd_kp.hip, dQ by fp32 atomics) ----
+# ---- key-block-parallel fused backward (csrc/flash_attn/fa_bwd_kp.hip, dQ by per-key-block fp32
+# slabs; fp32 atomics past 4 GiB of slabs or with CS336_FA_KP_SLAB=0) ----
 def _inputs_d(B, H, N, D, dt, seed=0):
     torch.manual_seed(seed)
     mk = lambda: torch.randn(B, N, H, D, device=DEV, dtype=dt).transpose(1, 2)  # noqa: E731
@@ -112,8 +113,10 @@ def _inputs_d(B, H, N, D, dt, seed=0):
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("N,D", [(64, 64), (256, 64), (320, 64), (512, 64), (1024, 64), (2048, 64),
                                  (64, 80), (320, 80), (1024, 80)])
-def test_kp_bwd_vs_fp64(dt, causal, N, D, monkeypatch):
+@pytest.mark.parametrize("waves", [4, 8])
+def test_kp_bwd_vs_fp64(dt, causal, N, D, waves, monkeypatch):
     monkeypatch.setenv("CS336_FA_BWD", "2")
+    monkeypatch.setenv("CS336_FA_KP_WAVES", str(waves))
     B, H = 2, 3
     q, k, v, do = _inputs_d(B, H, N, D, dt)
     hip = _hip()
@@ -129,8 +132,34 @@ def test_kp_bwd_vs_fp64(dt, causal, N, D, monkeypatch):
 
 
 @pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("N,D", [(320, 80), (1024, 80), (2048, 64)])
+def test_kp_slabs_vs_atomics(causal, N, D, monkeypatch):
+    """dQ summed from per-key-block slabs (default) equals the atomic accumulation up to fp32 add
+    order, is bitwise reproducible run to run, and leaves dK / dV bitwise unchanged."""
+    monkeypatch.setenv("CS336_FA_BWD", "2")
+    B, H = 2, 3
+    q, k, v, do = _inputs_d(B, H, N, D, torch.bfloat16, seed=5)
+    hip = _hip()
+    sc = D**-0.5
+    o, lse = hip.fa_fwd(q, k, v, causal, sc)
+    slab = hip.fa_bwd(do, q, k, v, o, lse, causal, sc)
+    again = hip.fa_bwd(do, q, k, v, o, lse, causal, sc)
+    monkeypatch.setenv("CS336_FA_KP_SLAB", "0")
+    atom = hip.fa_bwd(do, q, k, v, o, lse, causal, sc)
+    for a, b in zip(slab, again):
+        assert torch.equal(a, b)
+    assert torch.equal(slab[1], atom[1]) and torch.equal(slab[2], atom[2])
+    torch.testing.assert_close(slab[0].float(), atom[0].float(), rtol=1e-2, atol=1e-2)
+    rq, _, _ = _ref(q, k, v, do, causal)
+    for a in (slab[0], atom[0]):
+        err = (a.double() - rq).abs().max().item()
+        assert err <= 2e-2 * max(1.0, rq.abs().max().item())
+
+
+@pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("D", [64, 80])
-def test_kp_matches_two_kernel_long(causal, D, monkeypatch):
+@pytest.mark.parametrize("waves", [4, 8])
+def test_kp_matches_two_kernel_long(causal, D, waves, monkeypatch):
     """The reference FA benchmark's regime: few heads, long N (B·H 8, N 4096)."""
     B, H, N = 2, 4, 4096
     q, k, v, do = _inputs_d(B, H, N, D, torch.bfloat16, seed=3)
@@ -139,6 +168,7 @@ def test_kp_matches_two_kernel_long(causal, D, monkeypatch):
     monkeypatch.setenv("CS336_FA_BWD", "0")
     two = hip.fa_bwd(do, q, k, v, o, lse, causal, D**-0.5)
     monkeypatch.setenv("CS336_FA_BWD", "2")  # key-block parallel (the default only at d 80)
+    monkeypatch.setenv("CS336_FA_KP_WAVES", str(waves))
     kp = hip.fa_bwd(do, q, k, v, o, lse, causal, D**-0.5)
     for a, b in zip(kp, two):
         torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=2e-2)
