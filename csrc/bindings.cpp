@@ -254,7 +254,7 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
   //   unset: a head-sequential kernel where it applies and the (batch, head) workgroups fill the chip
   //          (B·H >= 512): fa_bwd_hs.hip (d 64, N <= 1024, N % 128 == 0), else fa_bwd_fused.hip
   //          (d 64, N <= 1024: the N % 128 == 64 shapes, 1.37x the two-kernel form,
-  //          profiles/r5_fa_bwd_forms.md); else at d 80 the key-block-parallel fused
+  //          profiles/r5_fa_bwd_forms.md); else at d 80 and long-N d 64 the key-block-parallel fused
   //          kernel (fa_bwd_kp.hip, dQ by slabs / fp32 atomics), else the two-kernel form (split over keys /
   //          queries at low parallelism);
   //   1: head-sequential wherever it applies (then as unset); 2: key-block parallel wherever it
@@ -324,10 +324,14 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
     }
     bp.dq_acc = nullptr;
   }
-  // key-block parallel: forced by mode 2; by default only at d 80 (the 2.7b model), where its 8-wave
-  // causal form beats the two-kernel form (B 32 H 32 N 1024 1.11 vs 1.35 ms, N 4096 617 vs 445 TF;
-  // profiles/r6_fa_kp_waves.md). At d 64 the two-kernel form stays ahead at N 4096 (r4_fa_kp.md, ibid.)
-  if ((mode == 2 || (mode < 0 && q.size(3) == 80)) && cs336::flash_attn_bwd_kp_ok(bp, to_dtype(q))) {
+  // key-block parallel: forced by mode 2; by default at d 80 (the 2.7b model: B 32 H 32 N 1024 causal
+  // 1.11 vs 1.35 ms for the two-kernel form, N 4096 617 vs 445 TF) and at d 64 for long sequences with
+  // at least 1024 key-block workgroups (N 4096 causal even, full 743 vs 701 TF, N 16384 causal 753 vs
+  // 719 TF); the 8-wave form, profiles/r6_fa_kp_waves.md. Below that (few heads: the two-kernel form
+  // splits keys / queries) and at N <= 1024 (head-sequential forms) it is not the default.
+  const bool kp_default = q.size(3) == 80 ||
+      (q.size(3) == 64 && q.size(2) >= 2048 && q.size(0) * q.size(1) * ((q.size(2) + 255) / 256) >= 1024);
+  if ((mode == 2 || (mode < 0 && kp_default)) && cs336::flash_attn_bwd_kp_ok(bp, to_dtype(q))) {
     at::Tensor ws = at::empty({(int64_t)cs336::flash_attn_bwd_kp_workspace(bp)}, q.options().dtype(at::kFloat));
     cs336::flash_attn_bwd_kp(bp, to_dtype(q), ws.data_ptr<float>(), stream());
     return;

@@ -22,7 +22,7 @@
 // (3) dQ = scale · (sum of the slabs | acc) cast to the output dtype (inverse RoPE folded in when q
 // was rotated).
 //
-// Main kernel structure: WV = 8 waves (two per SIMD, <= 256 registers each; the causal default) or 4
+// Main kernel structure: WV = 8 waves (two per SIMD, <= 256 registers each; the default) or 4
 // (one per SIMD, up to 512 registers), wave w owns 32 keys (8 waves) or 64 keys as two 32-key groups
 // (4 waves) of the block (key on the MFMA lane), keeping dKᵀ / dVᵀ of its keys and V (B operand of
 // dP) in registers; K lives in one LDS image read by rows (S) and by
@@ -48,12 +48,12 @@ constexpr int KP_BQ = 64;   // query slice
 constexpr int64_t KP_SLAB_LIMIT = (int64_t)4 << 30;  // bytes of dQ slabs before the atomic fallback
 
 // waves per workgroup: 4 (one per SIMD, 64 keys = two 32-key groups each) or 8 (two per SIMD, one group
-// each: a second wave on every SIMD covers the first one's LDS and barrier latencies). 8 under the
-// causal mask, 4 without it (there the d 80 8-wave build spills); CS336_FA_KP_WAVES=4|8 forces one.
-inline int kp_waves(const AttnBwdParams& bp) {
+// each: a second wave on every SIMD covers the first one's LDS and barrier latencies): 8 by default,
+// 1.15-1.45x the 4-wave form at every measured shape (profiles/r6_fa_kp_waves.md; the d 80 non-causal
+// build spills 13-15 registers and still wins); CS336_FA_KP_WAVES=4 selects the 4-wave form.
+inline int kp_waves(const AttnBwdParams&) {
   const char* e = getenv("CS336_FA_KP_WAVES");
-  if (e && *e) return atoi(e) == 8 ? 8 : 4;
-  return bp.f.causal ? 8 : 4;
+  return (e && *e && atoi(e) == 4) ? 4 : 8;
 }
 
 inline int kp_nkb(const AttnBwdParams& bp) { return (bp.f.Nq + KP_KB - 1) / KP_KB; }

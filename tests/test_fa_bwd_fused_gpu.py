@@ -134,9 +134,11 @@ def test_kp_bwd_vs_fp64(dt, causal, N, D, waves, monkeypatch):
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("N,D", [(320, 80), (1024, 80), (2048, 64)])
 def test_kp_slabs_vs_atomics(causal, N, D, monkeypatch):
-    """dQ summed from per-key-block slabs (default) equals the atomic accumulation up to fp32 add
-    order, is bitwise reproducible run to run, and leaves dK / dV bitwise unchanged."""
+    """dQ summed from per-key-block slabs (the default up to N 1024, forced here) equals the atomic
+    accumulation up to fp32 add order, is bitwise reproducible run to run, and leaves dK / dV bitwise
+    unchanged."""
     monkeypatch.setenv("CS336_FA_BWD", "2")
+    monkeypatch.setenv("CS336_FA_KP_SLAB", "1")
     B, H = 2, 3
     q, k, v, do = _inputs_d(B, H, N, D, torch.bfloat16, seed=5)
     hip = _hip()

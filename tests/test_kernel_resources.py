@@ -37,7 +37,10 @@ def test_no_scratch(src, tmp_path):
     scratch = [int(x) for x in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", r.stderr)]
     assert names and len(names) == len(scratch)
     # the forward's RoPE-on-load instantiations (fa_fwd_kernel<T, D, CAUSAL, ROPE=1, DMA=0>) are a
-    # fallback path the training step never takes (q/k arrive rotated by the QKV GEMM)
-    allowed = re.compile(r"fa_fwd_kernel.*Lb[01]ELb1ELi0E")
+    # fallback path the training step never takes (q/k arrive rotated by the QKV GEMM); the 8-wave
+    # key-block-parallel backward at d 80 without the causal mask (fa_bwd_kp_kernel<T, 80, false, ROPE,
+    # SLAB, 8>) spills 11-15 registers and still measures 1.43 vs 1.56 ms for the 4-wave form and 1.71
+    # for the two-kernel form at N 4096 (profiles/r6_fa_kp_waves.md); no training step runs it
+    allowed = re.compile(r"fa_fwd_kernel.*Lb[01]ELb1ELi0E|fa_bwd_kp_kernel.*Li80ELb0ELb[01]ELb[01]ELi8E")
     spills = [(n, s) for n, s in zip(names, scratch) if s and not allowed.search(n)]
     assert not spills, spills
