@@ -1,8 +1,9 @@
 // FlashAttention-2 backward, key-block parallel: ONE main kernel with the five MFMA products per
-// tile pair (S, dP, dVᵀ, dKᵀ, dQ), one workgroup per 256-key block, dQ summed across key blocks by
-// fp32 atomics. For the shapes the head-sequential fused kernel (fa_bwd_fused.hip: d 64, N <= 1024,
-// B·H >= 512) does not serve: long sequences with few heads (the reference's FA benchmark at
-// N 4096, B·H 64: 16 key blocks x 64 heads = 1024 workgroups) and d_head 80 (the 2.7b model).
+// tile pair (S, dP, dVᵀ, dKᵀ, dQ), one workgroup per 256-key block, dQ summed across key blocks
+// (slabs or fp32 atomics, below). For the shapes the head-sequential kernels (fa_bwd_hs.hip /
+// fa_bwd_fused.hip: d 64, N <= 1024, B·H >= 512) do not serve: d_head 80 (the 2.7b model) and long
+// d 64 sequences (the reference's FA benchmark at N 4096, B·H 64: 16 key blocks x 64 heads = 1024
+// workgroups; the leaderboard's N 16384).
 // cs336-build: no-slp
 //
 // Parity: reference cs336_systems/flash_attention.py:270-289 (recompute backward, there over the
