@@ -75,6 +75,7 @@ struct KpGeo {
   static constexpr int CPR = RB / 16;
   static constexpr int CREAL = D * 2 / 16;      // 16-B chunks with data
   static constexpr int NDT = DP / 32, NKS = DP / 16;
+  static constexpr int NKR = (D + 15) / 16;     // k-steps of S / dP over the real d (d 80: 5 of 6)
   static constexpr int TILE = KP_BQ * RB;       // one slice image
   static constexpr int SLOT = 2 * TILE + 1024;  // Q | dO | row constants (512 B used)
   static constexpr int NS = 3;
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(64 * WV, 1) void fa_bwd_kp_kernel(const AttnBwdPara
   constexpr int GPW = G::GPW;
   typedef typename Elem<T>::storage S;
   typedef typename Mma16<T>::frag F;
-  constexpr int DP = G::DP, RB = G::RB, NDT = G::NDT, NKS = G::NKS, CREAL = G::CREAL;
+  constexpr int DP = G::DP, RB = G::RB, NDT = G::NDT, NKS = G::NKS, NKR = G::NKR, CREAL = G::CREAL;
   __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
@@ -225,12 +226,12 @@ __global__ __launch_bounds__(64 * WV, 1) void fa_bwd_kp_kernel(const AttnBwdPara
 
   // ---- per-wave state: keys kw + 32g + l32, g < GPW ------------------------------------------------
   const int kw = kbase + 32 * GPW * wave;
-  uint4 vf[GPW][NKS];  // V as the B operand of dP (key on the lane), d = 16ks + 8hh .. +7
+  uint4 vf[GPW][NKR];  // V as the B operand of dP (key on the lane), d = 16ks + 8hh .. +7
 #pragma unroll
   for (int g = 0; g < GPW; ++g) {
     const int key = min(kw + 32 * g + l32, N - 1);  // keys >= N: whole skipped groups (N % 64 == 0)
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
+    for (int ks = 0; ks < NKR; ++ks) {
       const int d = 16 * ks + 8 * hh;
       vf[g][ks] = (DP == D || d < D) ? *reinterpret_cast<const uint4*>(Vp + (int64_t)key * bp.f.v_sn + d)
                                      : make_uint4(0, 0, 0, 0);
@@ -305,9 +306,9 @@ __global__ __launch_bounds__(64 * WV, 1) void fa_bwd_kp_kernel(const AttnBwdPara
       const char* dOt = dOs + 32 * t * RB;
       f32x16 sa[GPW], dp[GPW];
       {
-        F qa[NKS], oa[NKS];
+        F qa[NKR], oa[NKR];
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
+        for (int ks = 0; ks < NKR; ++ks) {
           qa[ks] = rowf(Qt, ks);
           oa[ks] = rowf(dOt, ks);
         }
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(64 * WV, 1) void fa_bwd_kp_kernel(const AttnBwdPara
           dp[g] = *reinterpret_cast<const f32x16*>(Ds + 32 * t + 16 * hh);
           sa[g] = zero16();
 #pragma unroll
-          for (int ks = 0; ks < NKS; ++ks) {
+          for (int ks = 0; ks < NKR; ++ks) {
             sa[g] = Mma16<T>::mma(qa[ks], rowf(Kg, ks), sa[g]);
             dp[g] = Mma16<T>::mma(oa[ks], as_frag<T>(vf[g][ks]), dp[g]);
           }

@@ -95,6 +95,9 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
 
   // ---- Q fragments (B operand), resident for the whole kernel -------------------------------
   constexpr int NQF = F32 ? DP / 8 : DP / 16;  // uint4 per lane
+  // 16-bit S = K Qᵀ reduces over the real d only: the 16-wide k-steps past D hold the zero pad
+  // (d 80: 5 of the 6 steps of the padded 96, d 16: 1 of 2)
+  constexpr int NKR = (D + 15) / 16;
   const Rope rope{p.rope_cos, p.rope_sin, D / 2};
   const int64_t* rpos = p.rope_pos ? p.rope_pos + (int64_t)b * p.Nq : nullptr;
   uint4 qf[NQF];
@@ -160,16 +163,16 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
     if constexpr (!F32 && DP <= 64) {
       // every K fragment of the tile read before the first MFMA (<= 32 VGPRs): the MFMA chain then
       // waits on one LDS round trip instead of one per fragment
-      typename Mma16<T>::frag kf[2][DP / 16];
+      typename Mma16<T>::frag kf[2][NKR];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int ks = 0; ks < DP / 16; ++ks) kf[t][ks] = lds_row_frag<T, RB>(Ks, 32 * t, ks, lane);
+        for (int ks = 0; ks < NKR; ++ks) kf[t][ks] = lds_row_frag<T, RB>(Ks, 32 * t, ks, lane);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         s[t] = zero16();
 #pragma unroll
-        for (int ks = 0; ks < DP / 16; ++ks) s[t] = Mma16<T>::mma(kf[t][ks], as_frag<T>(qf[ks]), s[t]);
+        for (int ks = 0; ks < NKR; ++ks) s[t] = Mma16<T>::mma(kf[t][ks], as_frag<T>(qf[ks]), s[t]);
       }
       return;
     }
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(256, (fwd_min_waves<T, D, CAUSAL, DMA>())) void fa_
         }
       } else {
 #pragma unroll
-        for (int ks = 0; ks < DP / 16; ++ks)
+        for (int ks = 0; ks < NKR; ++ks)
           s[t] = Mma16<T>::mma(lds_row_frag<T, RB>(Ks, 32 * t, ks, lane), as_frag<T>(qf[ks]), s[t]);
       }
     }
