@@ -176,6 +176,26 @@ def test_kp_matches_two_kernel_long(causal, D, waves, monkeypatch):
         torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("causal", [True, False])
+def test_default_long_d64_selects_kp(causal, monkeypatch):
+    """At d 64, N >= 2048 with >= 1024 key-block workgroups the default backward is the 8-wave
+    key-block-parallel kernel (csrc/bindings.cpp): it must match the two-kernel form there."""
+    B, H, N, D = 4, 16, 4096, 64
+    q, k, v, do = _inputs_d(B, H, N, D, torch.bfloat16, seed=6)
+    hip = _hip()
+    o, lse = hip.fa_fwd(q, k, v, causal, D**-0.5)
+    monkeypatch.delenv("CS336_FA_BWD", raising=False)
+    default = hip.fa_bwd(do, q, k, v, o, lse, causal, D**-0.5)
+    monkeypatch.setenv("CS336_FA_BWD", "2")
+    kp = hip.fa_bwd(do, q, k, v, o, lse, causal, D**-0.5)
+    monkeypatch.setenv("CS336_FA_BWD", "0")
+    two = hip.fa_bwd(do, q, k, v, o, lse, causal, D**-0.5)
+    for a, b, c in zip(default, kp, two):
+        # dK / dV have no atomics: the default is the key-block-parallel kernel bit for bit
+        torch.testing.assert_close(a.float(), c.float(), rtol=2e-2, atol=2e-2)
+    assert torch.equal(default[1], kp[1]) and torch.equal(default[2], kp[2])
+
+
 @pytest.mark.parametrize("D", [64, 80])
 def test_kp_rope_out_only_in_step_layout(D, monkeypatch):
     """The 2.7b step's call shape: strided views of one fused d(qkv) buffer, q/k already rotated,

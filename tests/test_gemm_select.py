@@ -78,3 +78,17 @@ def test_multi_rank_replaces_hipblaslt_table_pick(monkeypatch):
     monkeypatch.setattr(gemm, "_multi_rank", lambda: True)
     monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
     assert gemm._pick("nt", a, b, None, {"blas": lambda: None, "cs336": lambda: None}) == "cs336"
+
+
+def test_committed_table_has_no_hipblaslt_pick_for_xl_and_2p7b():
+    """The XL (52,224-token) and 2.7b (32,768-token) training steps run no hipBLASLt GEMM: every
+    committed pick for their projection problems is a cs336 kernel (gemm8 or a split-K plan), so one
+    GPU and multi-rank runs take the same kernels (profiles/r6_gemm_2p7b_g8.md)."""
+    import json
+    import os
+
+    doc = json.load(open(gemm.TABLE_FILE))
+    picks = {k: v for k, v in doc["entries"].items() if "(52224, " in k or "(32768, " in k}
+    assert picks
+    assert not {k: v for k, v in picks.items() if v in ("lt", "blas")}, "hipBLASLt pick in a training-step problem"
+    assert os.path.basename(gemm.TABLE_FILE) == "gemm_table_mi355x.json"
