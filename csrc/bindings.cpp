@@ -325,12 +325,13 @@ void fa_bwd_run(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k
     bp.dq_acc = nullptr;
   }
   // key-block parallel: forced by mode 2; by default at d 80 (the 2.7b model: B 32 H 32 N 1024 causal
-  // 1.11 vs 1.35 ms for the two-kernel form, N 4096 617 vs 445 TF) and at d 64 for long sequences with
-  // at least 1024 key-block workgroups (N 4096 causal even, full 743 vs 701 TF, N 16384 causal 753 vs
+  // 1.11 vs 1.35 ms for the two-kernel form, N 4096 617 vs 445 TF) and at d 64 for N >= 2048 with at
+  // least 512 key-block workgroups (N 2048 causal even, full 679 vs 654-674 TF; N 4096 causal even,
+  // full 744 vs 701; B 1 H 16 N 8192 684-687 vs 652 causal, 755-760 vs 726 full; N 16384 causal 753 vs
   // 719 TF); the 8-wave form, profiles/r6_fa_kp_waves.md. Below that (few heads: the two-kernel form
   // splits keys / queries) and at N <= 1024 (head-sequential forms) it is not the default.
   const bool kp_default = q.size(3) == 80 ||
-      (q.size(3) == 64 && q.size(2) >= 2048 && q.size(0) * q.size(1) * ((q.size(2) + 255) / 256) >= 1024);
+      (q.size(3) == 64 && q.size(2) >= 2048 && q.size(0) * q.size(1) * ((q.size(2) + 255) / 256) >= 512);
   if ((mode == 2 || (mode < 0 && kp_default)) && cs336::flash_attn_bwd_kp_ok(bp, to_dtype(q))) {
     at::Tensor ws = at::empty({(int64_t)cs336::flash_attn_bwd_kp_workspace(bp)}, q.options().dtype(at::kFloat));
     cs336::flash_attn_bwd_kp(bp, to_dtype(q), ws.data_ptr<float>(), stream());

@@ -178,7 +178,7 @@ def test_kp_matches_two_kernel_long(causal, D, waves, monkeypatch):
 
 @pytest.mark.parametrize("causal", [True, False])
 def test_default_long_d64_selects_kp(causal, monkeypatch):
-    """At d 64, N >= 2048 with >= 1024 key-block workgroups the default backward is the 8-wave
+    """At d 64, N >= 2048 with >= 512 key-block workgroups the default backward is the 8-wave
     key-block-parallel kernel (csrc/bindings.cpp): it must match the two-kernel form there."""
     B, H, N, D = 4, 16, 4096, 64
     q, k, v, do = _inputs_d(B, H, N, D, torch.bfloat16, seed=6)
