@@ -14,11 +14,21 @@ python - "$TAG" <<'P'
 import csv, glob, json, statistics, sys
 tag = sys.argv[1]
 res = {}
+
+
+def kind(n):
+    for key, name in (("kp", "fa_bwd_kp_kernel"), ("kp_prep", "fa_bwd_kp_prep"), ("kp_dq", "fa_bwd_kp_dq"),
+                      ("dq", "fa_bwd_dq"), ("dkdv", "fa_bwd_dkdv"), ("fused", "fa_bwd_fused"),
+                      ("hs", "fa_bwd_hs_kernel"), ("hs_prep", "fa_bwd_hs_prep")):
+        if name in n:
+            return key
+    return None
+
 for f in glob.glob(f"gpurun_out/pmc_{tag}/p*/**/*counter_collection.csv", recursive=True):
     vals = {}
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        k = "dq" if "fa_bwd_dq" in n else ("dkdv" if "fa_bwd_dkdv" in n else ("fused" if "fa_bwd_fused" in n else ("hs" if "fa_bwd_hs_kernel" in n else ("hs_prep" if "fa_bwd_hs_prep" in n else None))))
+        k = kind(n)
         if not k: continue
         vals.setdefault((k, r["Counter_Name"]), {}).setdefault(r["Dispatch_Id"], 0.0)
         vals[(k, r["Counter_Name"])][r["Dispatch_Id"]] += float(r["Counter_Value"])
@@ -28,14 +38,14 @@ for f in glob.glob(f"gpurun_out/pmc_{tag}/kt/**/*kernel_trace.csv", recursive=Tr
     ts = {}
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        k = "dq" if "fa_bwd_dq" in n else ("dkdv" if "fa_bwd_dkdv" in n else ("fused" if "fa_bwd_fused" in n else ("hs" if "fa_bwd_hs_kernel" in n else ("hs_prep" if "fa_bwd_hs_prep" in n else None))))
+        k = kind(n)
         if k: ts.setdefault(k, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     for k, v in ts.items():
         res.setdefault(k, {})["duration_us_median"] = statistics.median(v)
 for k, d in res.items():
-    if "SQ_INSTS_VALU" in d and "SQ_INSTS_MFMA" in d:
+    if d.get("SQ_INSTS_MFMA"):
         d["valu_per_mfma"] = d["SQ_INSTS_VALU"] / d["SQ_INSTS_MFMA"]
-    if "SQ_WAVE_CYCLES" in d:
+    if d.get("SQ_WAVE_CYCLES"):
         for c in ("SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"):
             if c in d: d[c + "/WAVE_CYCLES"] = d[c] / d["SQ_WAVE_CYCLES"]
 json.dump(res, open(f"gpurun_out/fa_bwd_pmc_{tag}.json", "w"), indent=1)
