@@ -15,7 +15,9 @@ from __future__ import annotations
 
 import datetime
 import os
+import random
 import socket
+import time
 from collections.abc import Callable
 
 import torch
@@ -25,7 +27,32 @@ import torch.multiprocessing as mp
 from .affinity import pin_rank_to_gpu
 
 
+def _ephemeral_low() -> int:
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as fh:
+            return int(fh.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        return 32768
+
+
 def find_free_port() -> int:
+    """A bindable TCP port on 127.0.0.1 for a rendezvous store, picked BELOW the kernel's ephemeral
+    range. A port from ``bind(0)`` is ephemeral: between this probe and the store's bind (seconds of
+    ``import torch`` in spawned ranks) the kernel may hand it to any outgoing connection on the box
+    (RCCL bootstrap, gloo pairs, other jobs) and the store fails with EADDRINUSE -- seen once in the
+    GPU suite. Ports below the range are only taken by explicit binds, so a random one that binds now
+    stays free. Falls back to ``bind(0)`` if no such port binds."""
+    lo = _ephemeral_low()
+    rng = random.Random(os.getpid() ^ time.time_ns())
+    if lo > 12000:
+        for _ in range(64):
+            port = rng.randrange(10000, lo)
+            with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+                try:
+                    s.bind(("127.0.0.1", port))
+                except OSError:
+                    continue
+                return port
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]

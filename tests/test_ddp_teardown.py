@@ -12,11 +12,26 @@ import torch.distributed as dist
 
 import cs336_systems.bench.ddp as bench_ddp
 from cs336_systems.models.transformer import BasicsTransformerLM
+from cs336_systems.parallel.comm import _ephemeral_low, find_free_port
+
+
+def test_find_free_port_is_outside_the_ephemeral_range():
+    """Rendezvous ports come from below the kernel's ephemeral range, so no outgoing connection can
+    take one between the probe and the store's bind (an EADDRINUSE seen in the GPU suite)."""
+    import socket
+
+    lo = _ephemeral_low()
+    for _ in range(8):
+        port = find_free_port()
+        if lo > 12000:
+            assert 10000 <= port < lo
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            s.bind(("127.0.0.1", port))
 
 
 def test_sweep_frees_every_model(monkeypatch):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = "29671"
+    os.environ["MASTER_PORT"] = str(find_free_port())
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
         refs = []
