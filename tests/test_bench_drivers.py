@@ -54,3 +54,21 @@ def test_ddp_overlap_name_is_working_overlapped_ddp():
     from cs336_systems.parallel import DDPIndividual
 
     assert DDPOverlap is DDPIndividual
+
+
+def test_reference_ddp_script_switches():
+    """The reference script's switches (ddp_bucketed_overlapped_sharded.py:366-419) map onto the
+    bench.ddp driver with the reference hyper-parameters; later options override them."""
+    from cs336_systems.ddp_bucketed_overlapped_sharded import reference_argv
+
+    def parsed(argv):
+        return ddp.parse(reference_argv(argv))
+
+    a = parsed([])
+    assert (a.variant, a.world_size, a.size, a.ctx, a.batch, a.lr, a.wd, a.steps) == ("naive", 1, "small", 128, 128, 1e-3, 0.1, 50)
+    assert (parsed(["--distributed"]).variant, parsed(["--ddp"]).variant) == ("naive", "individual")
+    b = parsed(["--ddp_bucketed", "--sharded", "--size", "tiny"])
+    assert (b.variant, b.sharded, b.world_size, b.size) == ("bucketed", True, 2, "tiny")
+    assert not parsed(["--distributed", "--sharded"]).sharded  # the reference shards under its DDP wrappers only
+    ddp.main(reference_argv(["--ddp_bucketed", "--sharded", "--cpu", "--size", "tiny", "--ctx", "32", "--batch", "4",
+                             "--steps", "2", "--warmup", "1", "--check"]))
